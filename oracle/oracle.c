@@ -1,0 +1,659 @@
+/*
+ * oracle.c — CPU restatement of the reference SpGEMM path. TEST INFRASTRUCTURE ONLY
+ * (parity checker + bench.py cpu_baseline). See oracle.h for the file:line map.
+ * Plain C11 + pthreads; built by oracle/Makefile into oracle/liboracle.so.
+ */
+#include "oracle.h"
+
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------ */
+/* ChaCha12 StdRng (rand 0.9.2 / rand_chacha 0.9.0 / rand_core 0.9.5, Cargo.lock:851-895).    */
+/* Key = seed as 8 LE words; words 12-13 = 64-bit block counter from 0; words 14-15 = stream 0. */
+/* rand_chacha refills 4 blocks (64 words) at a time; next_u64 = lo | hi << 32 of consecutive  */
+/* words. Only u64 draws are made on the reference's path, so the read index stays even.      */
+/* ------------------------------------------------------------------------------------------ */
+#define ROTL(x, n) (((x) << (n)) | ((x) >> (32 - (n))))
+#define QR(a, b, c, d)                                                                             \
+    a += b; d ^= a; d = ROTL(d, 16);                                                              \
+    c += d; b ^= c; b = ROTL(b, 12);                                                              \
+    a += b; d ^= a; d = ROTL(d, 8);                                                               \
+    c += d; b ^= c; b = ROTL(b, 7);
+
+void orc_chacha12_block(const uint32_t key[8], uint64_t counter, uint32_t out[16]) {
+    uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    for (int i = 0; i < 8; ++i) s[4 + i] = key[i];
+    s[12] = (uint32_t)counter;
+    s[13] = (uint32_t)(counter >> 32);
+    s[14] = 0;
+    s[15] = 0;
+    uint32_t x[16];
+    memcpy(x, s, sizeof x);
+    for (int r = 0; r < 6; ++r) { /* 12 rounds = 6 double rounds */
+        QR(x[0], x[4], x[8], x[12]);
+        QR(x[1], x[5], x[9], x[13]);
+        QR(x[2], x[6], x[10], x[14]);
+        QR(x[3], x[7], x[11], x[15]);
+        QR(x[0], x[5], x[10], x[15]);
+        QR(x[1], x[6], x[11], x[12]);
+        QR(x[2], x[7], x[8], x[13]);
+        QR(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + s[i];
+}
+
+void orc_rng_seed(orc_rng *r, const uint8_t seed[32]) {
+    for (int i = 0; i < 8; ++i)
+        r->key[i] = (uint32_t)seed[4 * i] | ((uint32_t)seed[4 * i + 1] << 8) |
+                    ((uint32_t)seed[4 * i + 2] << 16) | ((uint32_t)seed[4 * i + 3] << 24);
+    r->counter = 0;
+    r->idx = 64;
+}
+
+static void orc_rng_refill(orc_rng *r) {
+    for (int b = 0; b < 4; ++b) orc_chacha12_block(r->key, r->counter + (uint64_t)b, r->buf + 16 * b);
+    r->counter += 4;
+    r->idx = 0;
+}
+
+uint64_t orc_rng_next_u64(orc_rng *r) {
+    if (r->idx >= 64) orc_rng_refill(r);
+    uint64_t lo = r->buf[r->idx], hi = r->buf[r->idx + 1];
+    r->idx += 2;
+    return lo | (hi << 32);
+}
+
+/* rand 0.9 `random_range(0.0..1.0)` for f64: value1_2 - 1.0 with 52 random mantissa bits. */
+double orc_rng_next_f64(orc_rng *r) {
+    return (double)(orc_rng_next_u64(r) >> 12) * (1.0 / 4503599627370496.0);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* CSR helpers                                                                                */
+/* ------------------------------------------------------------------------------------------ */
+static size_t vsize(int dtype) { return dtype == ORC_U32 ? 4 : 8; }
+
+void orc_csr_free(orc_csr *m) {
+    if (!m) return;
+    free(m->row_ptr);
+    free(m->col);
+    free(m->val);
+    m->row_ptr = NULL;
+    m->col = NULL;
+    m->val = NULL;
+    m->nnz = 0;
+}
+
+typedef struct {
+    uint64_t key; /* row << 32 | col */
+    uint64_t v;   /* value bits (u32 / u64 / f64) */
+} trip;
+
+static int trip_cmp(const void *a, const void *b) {
+    uint64_t x = ((const trip *)a)->key, y = ((const trip *)b)->key;
+    return (x > y) - (x < y);
+}
+
+/* CsrMatrix::from_coo (src/graph_csr.rs:83-129): sort by (r,c), merge duplicates by summing
+ * (plain `+=`, wrapping in a release build), drop zero values. */
+static int from_trips(uint64_t n, trip *t, uint64_t nt, int dtype, orc_csr *out) {
+    qsort(t, nt, sizeof(trip), trip_cmp);
+    uint64_t nd = 0;
+    for (uint64_t i = 0; i < nt; ++i) {
+        if (nd > 0 && t[nd - 1].key == t[i].key) {
+            if (dtype == ORC_F64) {
+                double a, b;
+                memcpy(&a, &t[nd - 1].v, 8);
+                memcpy(&b, &t[i].v, 8);
+                a += b;
+                memcpy(&t[nd - 1].v, &a, 8);
+            } else if (dtype == ORC_U32) {
+                t[nd - 1].v = (uint32_t)(t[nd - 1].v + t[i].v);
+            } else {
+                t[nd - 1].v += t[i].v;
+            }
+        } else {
+            t[nd++] = t[i];
+        }
+    }
+    out->n = n;
+    out->dtype = dtype;
+    out->row_ptr = (uint64_t *)calloc(n + 1, 8);
+    out->col = (uint32_t *)malloc((nd ? nd : 1) * 4);
+    out->val = malloc((nd ? nd : 1) * vsize(dtype));
+    if (!out->row_ptr || !out->col || !out->val) return -1;
+    uint64_t k = 0, cur = 0;
+    for (uint64_t i = 0; i < nd; ++i) {
+        int zero;
+        if (dtype == ORC_F64) {
+            double a;
+            memcpy(&a, &t[i].v, 8);
+            zero = (a == 0.0);
+        } else {
+            zero = (t[i].v == 0);
+        }
+        if (zero) continue;
+        uint64_t r = t[i].key >> 32;
+        while (cur <= r) out->row_ptr[cur++] = k;
+        out->col[k] = (uint32_t)t[i].key;
+        if (dtype == ORC_U32)
+            ((uint32_t *)out->val)[k] = (uint32_t)t[i].v;
+        else
+            ((uint64_t *)out->val)[k] = t[i].v;
+        ++k;
+    }
+    while (cur <= n) out->row_ptr[cur++] = k;
+    out->nnz = k;
+    return 0;
+}
+
+int orc_from_coo(uint64_t n, uint64_t ntrip, const uint32_t *rows, const uint32_t *cols,
+                 const void *vals, int dtype, orc_csr *out) {
+    trip *t = (trip *)malloc((ntrip ? ntrip : 1) * sizeof(trip));
+    if (!t) return -1;
+    for (uint64_t i = 0; i < ntrip; ++i) {
+        t[i].key = ((uint64_t)rows[i] << 32) | cols[i];
+        if (dtype == ORC_U32)
+            t[i].v = ((const uint32_t *)vals)[i];
+        else
+            memcpy(&t[i].v, (const uint8_t *)vals + 8 * i, 8);
+    }
+    int rc = from_trips(n, t, ntrip, dtype, out);
+    free(t);
+    return rc;
+}
+
+/* CsrMatrix::lattice (src/graph_csr.rs:177-222): row-major strides, 3^d offsets decoded base-3
+ * with dimension 0 as the least-significant digit, self excluded, torus wraps with rem_euclid. */
+int orc_lattice(const uint64_t *dims, int ndim, int torus, orc_csr *out) {
+    uint64_t total = 1;
+    for (int d = 0; d < ndim; ++d) total *= dims[d];
+    uint64_t strides[16];
+    if (ndim > 16) return -1;
+    for (int d = 0; d < ndim; ++d) strides[d] = 1;
+    for (int d = ndim - 2; d >= 0; --d) strides[d] = strides[d + 1] * dims[d + 1];
+    uint64_t nnb = 1;
+    for (int d = 0; d < ndim; ++d) nnb *= 3;
+    trip *t = (trip *)malloc((total * nnb > 0 ? total * nnb : 1) * sizeof(trip));
+    if (!t) return -1;
+    uint64_t nt = 0;
+    uint64_t coord[16] = {0};
+    for (uint64_t node = 0; node < total; ++node) {
+        for (uint64_t off = 0; off < nnb; ++off) {
+            uint64_t tmp = off, neighbor = 0;
+            int all_zero = 1, valid = 1;
+            for (int d = 0; d < ndim; ++d) {
+                int64_t delta = (int64_t)(tmp % 3) - 1;
+                tmp /= 3;
+                if (delta != 0) all_zero = 0;
+                int64_t c = (int64_t)coord[d] + delta;
+                if (torus) {
+                    int64_t m = (int64_t)dims[d];
+                    c = ((c % m) + m) % m;
+                } else if (c < 0 || c >= (int64_t)dims[d]) {
+                    valid = 0;
+                    break;
+                }
+                neighbor += (uint64_t)c * strides[d];
+            }
+            if (all_zero || !valid) continue;
+            t[nt].key = (node << 32) | neighbor;
+            t[nt].v = 1;
+            ++nt;
+        }
+        for (int d = ndim - 1; d >= 0; --d) {
+            coord[d] += 1;
+            if (coord[d] < dims[d]) break;
+            coord[d] = 0;
+        }
+    }
+    int rc = from_trips(total, t, nt, ORC_U32, out);
+    free(t);
+    return rc;
+}
+
+static uint64_t get_bits(const orc_csr *m, uint64_t r, uint32_t c) {
+    uint64_t lo = m->row_ptr[r], hi = m->row_ptr[r + 1];
+    while (lo < hi) {
+        uint64_t mid = lo + (hi - lo) / 2;
+        if (m->col[mid] < c)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    if (lo < m->row_ptr[r + 1] && m->col[lo] == c) {
+        if (m->dtype == ORC_U32) return ((uint32_t *)m->val)[lo];
+        return ((uint64_t *)m->val)[lo];
+    }
+    return 0;
+}
+
+/* CsrMatrix::thin (src/graph_csr.rs:225-247): row-major scan; one f64 draw only when r <= c
+ * (the `&&` short-circuits), keep (r,c) and mirror (c,r) if present. */
+int orc_thin(const orc_csr *m, orc_rng *rng, double density, orc_csr *out) {
+    trip *t = (trip *)malloc((m->nnz ? m->nnz : 1) * sizeof(trip));
+    if (!t) return -1;
+    uint64_t nt = 0;
+    for (uint64_t r = 0; r < m->n; ++r) {
+        for (uint64_t idx = m->row_ptr[r]; idx < m->row_ptr[r + 1]; ++idx) {
+            uint32_t c = m->col[idx];
+            uint64_t v = m->dtype == ORC_U32 ? ((uint32_t *)m->val)[idx] : ((uint64_t *)m->val)[idx];
+            if (r <= c && orc_rng_next_f64(rng) < density) {
+                t[nt].key = (r << 32) | c;
+                t[nt].v = v;
+                ++nt;
+                if (r != c) {
+                    uint64_t rev = get_bits(m, c, (uint32_t)r);
+                    if (rev > 0) {
+                        t[nt].key = ((uint64_t)c << 32) | r;
+                        t[nt].v = rev;
+                        ++nt;
+                    }
+                }
+            }
+        }
+    }
+    int rc = from_trips(m->n, t, nt, m->dtype, out);
+    free(t);
+    return rc;
+}
+
+/* Value-type conversion (u32 -> Sat64 / f64), used to feed the same structure to every path. */
+int orc_convert(const orc_csr *m, int dtype, orc_csr *out) {
+    out->n = m->n;
+    out->nnz = m->nnz;
+    out->dtype = dtype;
+    out->row_ptr = (uint64_t *)malloc((m->n + 1) * 8);
+    out->col = (uint32_t *)malloc((m->nnz ? m->nnz : 1) * 4);
+    out->val = malloc((m->nnz ? m->nnz : 1) * vsize(dtype));
+    if (!out->row_ptr || !out->col || !out->val) return -1;
+    memcpy(out->row_ptr, m->row_ptr, (m->n + 1) * 8);
+    memcpy(out->col, m->col, m->nnz * 4);
+    for (uint64_t i = 0; i < m->nnz; ++i) {
+        uint64_t u;
+        double f;
+        if (m->dtype == ORC_U32) {
+            u = ((uint32_t *)m->val)[i];
+            f = (double)u;
+        } else if (m->dtype == ORC_SAT64) {
+            u = ((uint64_t *)m->val)[i];
+            f = (double)u;
+        } else {
+            f = ((double *)m->val)[i];
+            u = (uint64_t)f;
+        }
+        if (dtype == ORC_U32)
+            ((uint32_t *)out->val)[i] = (uint32_t)u;
+        else if (dtype == ORC_SAT64)
+            ((uint64_t *)out->val)[i] = u;
+        else
+            ((double *)out->val)[i] = f;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Semiring scalars: sadd/smul (src/graph_csr.rs:29-37), Sat64 (src/graph_sprs.rs:29-51),     */
+/* f64 plain +,* (linalg/src/csr.rs:81-85).                                                    */
+/* ------------------------------------------------------------------------------------------ */
+static inline uint32_t sadd32(uint32_t a, uint32_t b) {
+    uint32_t s = a + b;
+    return s < a ? 0xFFFFFFFFu : s;
+}
+static inline uint32_t smul32(uint32_t a, uint32_t b) {
+    uint64_t p = (uint64_t)a * b;
+    return p > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)p;
+}
+static inline uint64_t sadd64(uint64_t a, uint64_t b) {
+    uint64_t s = a + b;
+    return s < a ? ~0ull : s;
+}
+static inline uint64_t smul64(uint64_t a, uint64_t b) {
+    unsigned __int128 p = (unsigned __int128)a * b;
+    return (p >> 64) ? ~0ull : (uint64_t)p;
+}
+
+/* Small in-place unstable sort of u32 (stand-in for Rust's sort_unstable on nz_cols). */
+static void sort_u32(uint32_t *a, int64_t n) {
+    while (n > 24) {
+        uint32_t x = a[0], y = a[n / 2], z = a[n - 1];
+        uint32_t p = x < y ? (y < z ? y : (x < z ? z : x)) : (x < z ? x : (y < z ? z : y));
+        int64_t i = 0, j = n - 1;
+        for (;;) {
+            while (a[i] < p) ++i;
+            while (a[j] > p) --j;
+            if (i >= j) break;
+            uint32_t t = a[i];
+            a[i] = a[j];
+            a[j] = t;
+            ++i;
+            --j;
+        }
+        /* recurse on the smaller half, loop on the larger */
+        if (j + 1 < n - (j + 1)) {
+            sort_u32(a, j + 1);
+            a += j + 1;
+            n -= j + 1;
+        } else {
+            sort_u32(a + j + 1, n - (j + 1));
+            n = j + 1;
+        }
+    }
+    for (int64_t i = 1; i < n; ++i) {
+        uint32_t v = a[i];
+        int64_t j = i - 1;
+        while (j >= 0 && a[j] > v) {
+            a[j + 1] = a[j];
+            --j;
+        }
+        a[j + 1] = v;
+    }
+}
+
+/* Append a column to nz_cols, growing it (explicit zero values can re-push a column). */
+#define NZ_PUSH(j)                                                                                 \
+    do {                                                                                           \
+        if (nz_len == nz_cap) {                                                                    \
+            nz_cap *= 2;                                                                           \
+            uint32_t *nz2_ = (uint32_t *)realloc(nz, nz_cap * 4);                                  \
+            if (!nz2_) abort();                                                                    \
+            nz = nz2_;                                                                             \
+        }                                                                                          \
+        nz[nz_len++] = (j);                                                                        \
+    } while (0)
+
+/* Growable output buffers for the sequential matmul. */
+typedef struct {
+    uint32_t *col;
+    uint8_t *val;
+    uint64_t len, cap;
+} obuf;
+
+static int obuf_push(obuf *o, uint32_t c, const void *v, size_t vs) {
+    if (o->len == o->cap) {
+        uint64_t nc = o->cap ? o->cap * 2 : 1024;
+        uint32_t *nc_ = (uint32_t *)realloc(o->col, nc * 4);
+        uint8_t *nv = (uint8_t *)realloc(o->val, nc * vs);
+        if (!nc_ || !nv) return -1;
+        o->col = nc_;
+        o->val = nv;
+        o->cap = nc;
+    }
+    o->col[o->len] = c;
+    memcpy(o->val + o->len * vs, v, vs);
+    o->len++;
+    return 0;
+}
+
+/* CsrMatrix::matmul (src/graph_csr.rs:306-346) — dense accumulator, nz_cols pushed when the
+ * accumulator is zero, sort_unstable, emit non-zero values, clear. Same loop for Sat64 and for
+ * linalg Csr<u32,f64>::matmul (linalg/src/csr.rs:308-356). */
+int orc_matmul_seq(const orc_csr *a, const orc_csr *b, orc_csr *out) {
+    if (a->n != b->n || a->dtype != b->dtype) return -2;
+    const uint64_t n = a->n;
+    const int dt = a->dtype;
+    const size_t vs = vsize(dt);
+    out->n = n;
+    out->dtype = dt;
+    out->row_ptr = (uint64_t *)malloc((n + 1) * 8);
+    uint8_t *acc = (uint8_t *)calloc(n ? n : 1, vs);
+    uint32_t *nz = (uint32_t *)malloc((n ? n : 1) * 4 * 2 + 64);
+    if (!out->row_ptr || !acc || !nz) return -1;
+    uint64_t nz_cap = (n ? n : 1) * 2 + 16, nz_len = 0; /* f64 may re-push a column */
+    obuf o = {0};
+    out->row_ptr[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        for (uint64_t idx = a->row_ptr[i]; idx < a->row_ptr[i + 1]; ++idx) {
+            uint32_t k = a->col[idx];
+            for (uint64_t jdx = b->row_ptr[k]; jdx < b->row_ptr[k + 1]; ++jdx) {
+                uint32_t j = b->col[jdx];
+                if (dt == ORC_U32) {
+                    uint32_t *ac = (uint32_t *)acc;
+                    if (ac[j] == 0) NZ_PUSH(j);
+                    ac[j] = sadd32(ac[j], smul32(((uint32_t *)a->val)[idx], ((uint32_t *)b->val)[jdx]));
+                } else if (dt == ORC_SAT64) {
+                    uint64_t *ac = (uint64_t *)acc;
+                    if (ac[j] == 0) NZ_PUSH(j);
+                    ac[j] = sadd64(ac[j], smul64(((uint64_t *)a->val)[idx], ((uint64_t *)b->val)[jdx]));
+                } else {
+                    double *ac = (double *)acc;
+                    if (ac[j] == 0.0) NZ_PUSH(j);
+                    double prod = ((double *)a->val)[idx] * ((double *)b->val)[jdx];
+                    ac[j] = ac[j] + prod;
+                }
+            }
+        }
+        sort_u32(nz, (int64_t)nz_len);
+        for (uint64_t q = 0; q < nz_len; ++q) {
+            uint32_t j = nz[q];
+            if (dt == ORC_U32) {
+                uint32_t v = ((uint32_t *)acc)[j];
+                if (v != 0 && obuf_push(&o, j, &v, 4)) return -1;
+                ((uint32_t *)acc)[j] = 0;
+            } else if (dt == ORC_SAT64) {
+                uint64_t v = ((uint64_t *)acc)[j];
+                if (v != 0 && obuf_push(&o, j, &v, 8)) return -1;
+                ((uint64_t *)acc)[j] = 0;
+            } else {
+                double v = ((double *)acc)[j];
+                if (v != 0.0 && obuf_push(&o, j, &v, 8)) return -1;
+                ((double *)acc)[j] = 0.0;
+            }
+        }
+        nz_len = 0;
+        out->row_ptr[i + 1] = o.len;
+    }
+    free(acc);
+    free(nz);
+    out->nnz = o.len;
+    out->col = o.col ? o.col : (uint32_t *)malloc(4);
+    out->val = o.val ? (void *)o.val : malloc(8);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* CsrMatrix::matmul_par (src/graph_csr.rs:350-484): pass 1 symbolic (bool mask), serial       */
+/* prefix sum, zeroed exact-size outputs, pass 2 numeric into disjoint row slices. rayon's      */
+/* work-stealing `par_iter` is replaced by a dynamic row-chunk scheduler over pthreads.         */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    const orc_csr *a, *b;
+    uint64_t *nnz_row;
+    uint64_t *row_ptr;
+    uint32_t *ocol;
+    uint8_t *oval;
+    atomic_uint_fast64_t next;
+    int pass;
+} par_job;
+
+#define PAR_CHUNK 64
+
+static void *par_worker(void *arg) {
+    par_job *J = (par_job *)arg;
+    const orc_csr *a = J->a, *b = J->b;
+    const uint64_t n = a->n;
+    const int dt = a->dtype;
+    const size_t vs = vsize(dt);
+    if (J->pass == 1) {
+        uint8_t *mask = (uint8_t *)calloc(n ? n : 1, 1);
+        for (;;) {
+            uint64_t r0 = atomic_fetch_add(&J->next, PAR_CHUNK);
+            if (r0 >= n) break;
+            uint64_t r1 = r0 + PAR_CHUNK < n ? r0 + PAR_CHUNK : n;
+            for (uint64_t i = r0; i < r1; ++i) {
+                uint64_t count = 0;
+                for (uint64_t idx = a->row_ptr[i]; idx < a->row_ptr[i + 1]; ++idx) {
+                    uint32_t k = a->col[idx];
+                    for (uint64_t jdx = b->row_ptr[k]; jdx < b->row_ptr[k + 1]; ++jdx) {
+                        uint32_t j = b->col[jdx];
+                        if (!mask[j]) {
+                            mask[j] = 1;
+                            ++count;
+                        }
+                    }
+                }
+                J->nnz_row[i] = count;
+                for (uint64_t idx = a->row_ptr[i]; idx < a->row_ptr[i + 1]; ++idx) {
+                    uint32_t k = a->col[idx];
+                    for (uint64_t jdx = b->row_ptr[k]; jdx < b->row_ptr[k + 1]; ++jdx) mask[b->col[jdx]] = 0;
+                }
+            }
+        }
+        free(mask);
+    } else {
+        uint8_t *acc = (uint8_t *)calloc(n ? n : 1, vs);
+        uint64_t nz_cap = (n ? n : 1) * 2 + 16;
+        uint32_t *nz = (uint32_t *)malloc(nz_cap * 4);
+        for (;;) {
+            uint64_t r0 = atomic_fetch_add(&J->next, PAR_CHUNK);
+            if (r0 >= n) break;
+            uint64_t r1 = r0 + PAR_CHUNK < n ? r0 + PAR_CHUNK : n;
+            for (uint64_t i = r0; i < r1; ++i) {
+                uint64_t nz_len = 0;
+                for (uint64_t idx = a->row_ptr[i]; idx < a->row_ptr[i + 1]; ++idx) {
+                    uint32_t k = a->col[idx];
+                    for (uint64_t jdx = b->row_ptr[k]; jdx < b->row_ptr[k + 1]; ++jdx) {
+                        uint32_t j = b->col[jdx];
+                        if (dt == ORC_U32) {
+                            uint32_t *ac = (uint32_t *)acc;
+                            if (ac[j] == 0) NZ_PUSH(j);
+                            ac[j] = sadd32(ac[j], smul32(((uint32_t *)a->val)[idx], ((uint32_t *)b->val)[jdx]));
+                        } else if (dt == ORC_SAT64) {
+                            uint64_t *ac = (uint64_t *)acc;
+                            if (ac[j] == 0) NZ_PUSH(j);
+                            ac[j] = sadd64(ac[j], smul64(((uint64_t *)a->val)[idx], ((uint64_t *)b->val)[jdx]));
+                        } else {
+                            double *ac = (double *)acc;
+                            if (ac[j] == 0.0) NZ_PUSH(j);
+                            ac[j] = ac[j] + ((double *)a->val)[idx] * ((double *)b->val)[jdx];
+                        }
+                    }
+                }
+                sort_u32(nz, (int64_t)nz_len);
+                uint64_t pos = J->row_ptr[i];
+                for (uint64_t q = 0; q < nz_len; ++q) {
+                    uint32_t j = nz[q];
+                    int nonzero;
+                    if (dt == ORC_F64)
+                        nonzero = ((double *)acc)[j] != 0.0;
+                    else if (dt == ORC_U32)
+                        nonzero = ((uint32_t *)acc)[j] != 0;
+                    else
+                        nonzero = ((uint64_t *)acc)[j] != 0;
+                    if (nonzero) {
+                        J->ocol[pos] = j;
+                        memcpy(J->oval + pos * vs, acc + (uint64_t)j * vs, vs);
+                        ++pos;
+                    }
+                    memset(acc + (uint64_t)j * vs, 0, vs);
+                }
+            }
+        }
+        free(acc);
+        free(nz);
+    }
+    return NULL;
+}
+
+int orc_matmul_par(const orc_csr *a, const orc_csr *b, int nthreads, orc_csr *out) {
+    if (a->n != b->n || a->dtype != b->dtype) return -2;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 1024) nthreads = 1024;
+    const uint64_t n = a->n;
+    par_job J;
+    J.a = a;
+    J.b = b;
+    J.nnz_row = (uint64_t *)calloc(n ? n : 1, 8);
+    J.pass = 1;
+    atomic_init(&J.next, 0);
+    pthread_t th[1024];
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, par_worker, &J);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    uint64_t *row_ptr = (uint64_t *)malloc((n + 1) * 8);
+    row_ptr[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) row_ptr[i + 1] = row_ptr[i] + J.nnz_row[i];
+    const uint64_t total = row_ptr[n];
+    const size_t vs = vsize(a->dtype);
+    J.row_ptr = row_ptr;
+    J.ocol = (uint32_t *)calloc(total ? total : 1, 4);
+    J.oval = (uint8_t *)calloc(total ? total : 1, vs);
+    J.pass = 2;
+    atomic_store(&J.next, 0);
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, par_worker, &J);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(J.nnz_row);
+    out->n = n;
+    out->nnz = total;
+    out->dtype = a->dtype;
+    out->row_ptr = row_ptr;
+    out->col = J.ocol;
+    out->val = J.oval;
+    return 0;
+}
+
+/* CsrMatrix::add (src/graph_csr.rs:487-542): per-row sorted merge; equal columns combine with
+ * sadd and are dropped if the sum is zero. */
+int orc_add(const orc_csr *a, const orc_csr *b, orc_csr *out) {
+    if (a->n != b->n || a->dtype != b->dtype) return -2;
+    const uint64_t n = a->n;
+    const int dt = a->dtype;
+    const size_t vs = vsize(dt);
+    out->n = n;
+    out->dtype = dt;
+    out->row_ptr = (uint64_t *)malloc((n + 1) * 8);
+    obuf o = {0};
+    out->row_ptr[0] = 0;
+    const uint8_t *av = (const uint8_t *)a->val, *bv = (const uint8_t *)b->val;
+    for (uint64_t r = 0; r < n; ++r) {
+        uint64_t ai = a->row_ptr[r], ae = a->row_ptr[r + 1], bi = b->row_ptr[r], be = b->row_ptr[r + 1];
+        while (ai < ae && bi < be) {
+            uint32_t ac = a->col[ai], bc = b->col[bi];
+            if (ac < bc) {
+                obuf_push(&o, ac, av + ai * vs, vs);
+                ++ai;
+            } else if (ac > bc) {
+                obuf_push(&o, bc, bv + bi * vs, vs);
+                ++bi;
+            } else {
+                uint8_t tmp[8];
+                int nz;
+                if (dt == ORC_U32) {
+                    uint32_t v = sadd32(((const uint32_t *)av)[ai], ((const uint32_t *)bv)[bi]);
+                    memcpy(tmp, &v, 4);
+                    nz = v != 0;
+                } else if (dt == ORC_SAT64) {
+                    uint64_t v = sadd64(((const uint64_t *)av)[ai], ((const uint64_t *)bv)[bi]);
+                    memcpy(tmp, &v, 8);
+                    nz = v != 0;
+                } else {
+                    double v = ((const double *)av)[ai] + ((const double *)bv)[bi];
+                    memcpy(tmp, &v, 8);
+                    nz = v != 0.0;
+                }
+                if (nz) obuf_push(&o, ac, tmp, vs);
+                ++ai;
+                ++bi;
+            }
+        }
+        for (; ai < ae; ++ai) obuf_push(&o, a->col[ai], av + ai * vs, vs);
+        for (; bi < be; ++bi) obuf_push(&o, b->col[bi], bv + bi * vs, vs);
+        out->row_ptr[r + 1] = o.len;
+    }
+    out->nnz = o.len;
+    out->col = o.col ? o.col : (uint32_t *)malloc(4);
+    out->val = o.val ? (void *)o.val : malloc(8);
+    return 0;
+}
+
+/* Number of scalar products of a*b (Σ_i Σ_{k∈A_i} nnz(B_k)). */
+uint64_t orc_flops(const orc_csr *a, const orc_csr *b) {
+    uint64_t f = 0;
+    for (uint64_t idx = 0; idx < a->nnz; ++idx) {
+        uint32_t k = a->col[idx];
+        f += b->row_ptr[k + 1] - b->row_ptr[k];
+    }
+    return f;
+}

@@ -1,0 +1,70 @@
+/*
+ * oracle.h — CPU restatement of the reference SpGEMM path. TEST INFRASTRUCTURE ONLY.
+ *
+ * This library is the parity checker and the `cpu_baseline` leg of bench.py. Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline may load it. The product path
+ * (libslat.so) never links or calls it.
+ *
+ * What it restates (reference = imlvts/sparse-linear-algebra-tests, read-only at /root/reference):
+ *   orc_rng_*        rand 0.9.2 StdRng = rand_chacha 0.9.0 ChaCha12Rng (Cargo.lock:851-895),
+ *                    f64 draws as rand's UniformFloat::sample_single: (next_u64 >> 12) * 2^-52.
+ *   orc_lattice      CsrMatrix::lattice          src/graph_csr.rs:177-222
+ *   orc_thin         CsrMatrix::thin             src/graph_csr.rs:225-247 (same draw pattern as
+ *                    SparseCountMatrix::thin, src/graph.rs:143-154)
+ *   orc_from_coo     CsrMatrix::from_coo         src/graph_csr.rs:83-129
+ *   orc_matmul_seq   CsrMatrix::matmul           src/graph_csr.rs:306-346   (u32 saturating)
+ *                    same algorithm on Sat64     src/graph_sprs.rs:15-86    (u64 saturating)
+ *                    linalg Csr<u32,f64>::matmul linalg/src/csr.rs:308-356  (f64, left fold)
+ *   orc_matmul_par   CsrMatrix::matmul_par       src/graph_csr.rs:350-484   (two-pass, threads)
+ *   orc_add          CsrMatrix::add              src/graph_csr.rs:487-542
+ *
+ * Parity pin: see tests/golden/ (nnz sequence that rounds to README.md:41-46, SHA-256 of the
+ * arrays computed independently by tests/golden/make_golden.py with numpy+scipy).
+ */
+#ifndef SLAT_ORACLE_H
+#define SLAT_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_U32 = 0, ORC_SAT64 = 1, ORC_F64 = 2 };
+
+typedef struct {
+    uint64_t n;        /* square n x n */
+    uint64_t nnz;
+    int32_t dtype;     /* ORC_U32 / ORC_SAT64 / ORC_F64 */
+    int32_t _pad;
+    uint64_t *row_ptr; /* n+1 */
+    uint32_t *col;     /* nnz */
+    void *val;         /* nnz x (4 | 8 | 8) bytes */
+} orc_csr;
+
+typedef struct {
+    uint32_t key[8];
+    uint64_t counter;  /* next block counter */
+    uint32_t buf[64];  /* 4 blocks, like rand_chacha's 4-block refill */
+    uint32_t idx;      /* next word in buf; 64 = empty */
+} orc_rng;
+
+void orc_rng_seed(orc_rng *r, const uint8_t seed[32]);
+uint64_t orc_rng_next_u64(orc_rng *r);
+double orc_rng_next_f64(orc_rng *r);
+void orc_chacha12_block(const uint32_t key[8], uint64_t counter, uint32_t out[16]);
+
+void orc_csr_free(orc_csr *m);
+int orc_from_coo(uint64_t n, uint64_t ntrip, const uint32_t *rows, const uint32_t *cols,
+                 const void *vals, int dtype, orc_csr *out);
+int orc_lattice(const uint64_t *dims, int ndim, int torus, orc_csr *out);
+int orc_thin(const orc_csr *m, orc_rng *rng, double density, orc_csr *out);
+int orc_convert(const orc_csr *m, int dtype, orc_csr *out);
+int orc_matmul_seq(const orc_csr *a, const orc_csr *b, orc_csr *out);
+int orc_matmul_par(const orc_csr *a, const orc_csr *b, int nthreads, orc_csr *out);
+int orc_add(const orc_csr *a, const orc_csr *b, orc_csr *out);
+uint64_t orc_flops(const orc_csr *a, const orc_csr *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

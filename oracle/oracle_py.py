@@ -1,0 +1,196 @@
+"""ctypes wrapper of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference SpGEMM path (see oracle.h for the reference file:line
+map). Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module; the product (sparse-linear-algebra-tests_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+U32, SAT64, F64 = 0, 1, 2
+_VDT = {U32: np.uint32, SAT64: np.uint64, F64: np.float64}
+
+
+class _Csr(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("nnz", C.c_uint64), ("dtype", C.c_int32), ("_pad", C.c_int32),
+                ("row_ptr", C.c_void_p), ("col", C.c_void_p), ("val", C.c_void_p)]
+
+
+class _Rng(C.Structure):
+    _fields_ = [("key", C.c_uint32 * 8), ("counter", C.c_uint64), ("buf", C.c_uint32 * 64),
+                ("idx", C.c_uint32)]
+
+
+def build() -> str:
+    """Compile liboracle.so with the committed Makefile (gcc only)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        P = C.POINTER
+        L.orc_rng_seed.argtypes = [P(_Rng), C.c_char_p]
+        L.orc_rng_next_u64.argtypes = [P(_Rng)]
+        L.orc_rng_next_u64.restype = C.c_uint64
+        L.orc_rng_next_f64.argtypes = [P(_Rng)]
+        L.orc_rng_next_f64.restype = C.c_double
+        L.orc_chacha12_block.argtypes = [P(C.c_uint32), C.c_uint64, P(C.c_uint32)]
+        L.orc_csr_free.argtypes = [P(_Csr)]
+        L.orc_from_coo.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                   P(_Csr)]
+        L.orc_lattice.argtypes = [P(C.c_uint64), C.c_int, C.c_int, P(_Csr)]
+        L.orc_thin.argtypes = [P(_Csr), P(_Rng), C.c_double, P(_Csr)]
+        L.orc_convert.argtypes = [P(_Csr), C.c_int, P(_Csr)]
+        L.orc_matmul_seq.argtypes = [P(_Csr), P(_Csr), P(_Csr)]
+        L.orc_matmul_par.argtypes = [P(_Csr), P(_Csr), C.c_int, P(_Csr)]
+        L.orc_add.argtypes = [P(_Csr), P(_Csr), P(_Csr)]
+        L.orc_flops.argtypes = [P(_Csr), P(_Csr)]
+        L.orc_flops.restype = C.c_uint64
+        _lib = L
+    return _lib
+
+
+class Rng:
+    """rand 0.9 StdRng (ChaCha12) restatement."""
+
+    def __init__(self, seed: bytes = bytes([42] * 32)):
+        assert len(seed) == 32
+        self._r = _Rng()
+        lib().orc_rng_seed(C.byref(self._r), seed)
+
+    def next_u64(self) -> int:
+        return lib().orc_rng_next_u64(C.byref(self._r))
+
+    def next_f64(self) -> float:
+        return lib().orc_rng_next_f64(C.byref(self._r))
+
+
+class Csr:
+    """Owned host CSR from the oracle (n x n, u64 row_ptr, u32 col, typed values)."""
+
+    def __init__(self, raw: _Csr):
+        self._raw = raw
+
+    def __del__(self):
+        if getattr(self, "_raw", None) is not None and _lib is not None:
+            _lib.orc_csr_free(C.byref(self._raw))
+            self._raw = None
+
+    @property
+    def n(self) -> int:
+        return int(self._raw.n)
+
+    @property
+    def nnz(self) -> int:
+        return int(self._raw.nnz)
+
+    @property
+    def dtype(self) -> int:
+        return int(self._raw.dtype)
+
+    def arrays(self):
+        """Copies of (row_ptr u64, col u32, values)."""
+        n, z = self.n, self.nnz
+        rp = np.ctypeslib.as_array(C.cast(self._raw.row_ptr, C.POINTER(C.c_uint64)), (n + 1,)).copy()
+        if z:
+            col = np.ctypeslib.as_array(C.cast(self._raw.col, C.POINTER(C.c_uint32)), (z,)).copy()
+            vt = _VDT[self.dtype]
+            ct = {np.uint32: C.c_uint32, np.uint64: C.c_uint64, np.float64: C.c_double}[vt]
+            val = np.ctypeslib.as_array(C.cast(self._raw.val, C.POINTER(ct)), (z,)).copy()
+        else:
+            col = np.zeros(0, np.uint32)
+            val = np.zeros(0, _VDT[self.dtype])
+        return rp, col, val
+
+    def get(self, r: int, c: int):
+        rp, col, val = self.arrays()
+        s, e = int(rp[r]), int(rp[r + 1])
+        i = int(np.searchsorted(col[s:e], c))
+        if i < e - s and col[s + i] == c:
+            return val[s + i].item()
+        return 0
+
+
+def _new(fn, *args) -> Csr:
+    out = _Csr()
+    rc = fn(*args, C.byref(out))
+    if rc != 0:
+        raise RuntimeError(f"oracle call failed rc={rc}")
+    return Csr(out)
+
+
+def from_coo(n: int, rows, cols, vals, dtype: int = U32) -> Csr:
+    rows = np.ascontiguousarray(rows, np.uint32)
+    cols = np.ascontiguousarray(cols, np.uint32)
+    vals = np.ascontiguousarray(vals, _VDT[dtype])
+    return _new(lib().orc_from_coo, n, len(rows), rows.ctypes.data, cols.ctypes.data, vals.ctypes.data, dtype)
+
+
+def from_edges(n: int, edges, dtype: int = U32) -> Csr:
+    e = np.asarray(edges, dtype=np.int64).reshape(-1, 2)
+    return from_coo(n, e[:, 0], e[:, 1], np.ones(len(e)), dtype)
+
+
+def from_arrays(row_ptr, col, val, dtype: int) -> Csr:
+    rp = np.asarray(row_ptr, np.uint64)
+    n = len(rp) - 1
+    rows = np.repeat(np.arange(n, dtype=np.uint32), np.diff(rp).astype(np.int64))
+    return from_coo(n, rows, col, val, dtype)
+
+
+def lattice(dims, torus: bool) -> Csr:
+    d = (C.c_uint64 * len(dims))(*dims)
+    return _new(lib().orc_lattice, d, len(dims), int(torus))
+
+
+def thin(m: Csr, rng: Rng, density: float) -> Csr:
+    return _new(lib().orc_thin, C.byref(m._raw), C.byref(rng._r), density)
+
+
+def convert(m: Csr, dtype: int) -> Csr:
+    return _new(lib().orc_convert, C.byref(m._raw), dtype)
+
+
+def matmul_seq(a: Csr, b: Csr) -> Csr:
+    return _new(lib().orc_matmul_seq, C.byref(a._raw), C.byref(b._raw))
+
+
+def matmul_par(a: Csr, b: Csr, nthreads: int) -> Csr:
+    return _new(lib().orc_matmul_par, C.byref(a._raw), C.byref(b._raw), nthreads)
+
+
+def add(a: Csr, b: Csr) -> Csr:
+    return _new(lib().orc_add, C.byref(a._raw), C.byref(b._raw))
+
+
+def flops(a: Csr, b: Csr) -> int:
+    return int(lib().orc_flops(C.byref(a._raw), C.byref(b._raw)))
+
+
+def identity(n: int, dtype: int = U32) -> Csr:
+    r = np.arange(n, dtype=np.uint32)
+    return from_coo(n, r, r, np.ones(n), dtype)
+
+
+def torus_thinned(side: int, epn: float, rng: Rng) -> Csr:
+    """The bench_repeated_exponentiation input: side^3 Moore torus thinned to `epn` edges/node
+    (src/graph_magnus.rs:707-719)."""
+    full = lattice([side, side, side], True)
+    density = epn / (full.nnz / full.n)
+    return thin(full, rng, density) if density < 1.0 else full
