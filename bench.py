@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""bench.py — GNNZ/s of the MI355X SpGEMM on the reference's headline workload.
+
+Workload (BASELINE.json configs[1], the one the metric is quoted on): the 30^3 Moore torus
+thinned to 3 edges/node with StdRng seed [42;32] (src/graph_magnus.rs:707-719), one step =
+C = A^6 · A (the A^7 step of bench_repeated_exponentiation, src/graph_magnus.rs:740-772), u32
+saturating values, nnz(C) = 11,736,555. Inputs are device-resident before the timed region; each
+step is one complete synchronous SpGEMM call (symbolic, scan, C allocation, numeric, nnz read-back)
+and its output is released inside the step.
+
+N > 1 (torchrun, one rank per GPU): `--scaling weak` (default) — the global matrix is the
+block-diagonal of N independent tori and rank r owns block r (1-D row partition, no data-path
+collective); `--scaling strong` — config C4, 100^3 torus A^3·A, rows split across ranks into
+flops-balanced blocks, B replicated. value = output nnz of all ranks / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sparse-linear-algebra-tests_amd"))
+
+import numpy as np  # noqa: E402
+
+import slat  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+README_CSR_PAR_A7_GNNZ = 11736555 / 40.5e-3 / 1e9   # README.md:46, unstated hardware: 0.290 GNNZ/s
+
+
+def algorithmic_bytes(nnz_a: int, nnz_b: int, nnz_c: int, n: int, vsize: int) -> int:
+    """compulsory traffic, each array touched once."""
+    return (4 + vsize) * (nnz_a + nnz_b + nnz_c) + 8 * 3 * (n + 1)
+
+
+def build_inputs(side: int, power: int, ctx):
+    A = slat.CsrMatrix.from_host(slat.torus_thinned(side, 3.0, slat.StdRng()), ctx)
+    P = A
+    for _ in range(2, power):
+        P = P.matmul(A)
+    return A, P
+
+
+def cpu_baseline(side: int, power: int, seconds: float = 12.0):
+    """Oracle restatement of CsrMatrix::matmul_par (oracle/, kind 'port') on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    A = O.torus_thinned(side, 3.0, O.Rng())
+    P = A
+    for _ in range(2, power):
+        P = O.matmul_seq(P, A)
+    C = O.matmul_par(P, A, threads)  # warm-up (reference: 1 warm-up + timed iterations)
+    nnz = C.nnz
+    del C
+    iters, t0 = 0, time.perf_counter()
+    while True:
+        O.matmul_par(P, A, threads)
+        iters += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and iters >= 3) or iters >= 200:
+            break
+    per = el / iters
+    return {"value": nnz / per / 1e9, "unit": "GNNZ/s", "cores": threads, "kind": "port",
+            "sample": f"A^{power - 1}*A on {side}^3 torus (nnz(C)={nnz}), {iters} timed calls after 1 warm-up, "
+                      f"{per * 1e3:.2f} ms/call, oracle/oracle.c orc_matmul_par with {threads} threads"}
+
+
+def load_pmc(workload: str):
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--side", type=int, default=30)
+    ap.add_argument("--power", type=int, default=7, help="C = A^(power-1) * A")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    ctx = slat.Context(local)
+    side, power = args.side, args.power
+    if args.scaling == "strong" and world > 1 and side == 30:
+        side, power = 100, 4
+    A, P = build_inputs(side, power, ctx)
+    n = A.n
+    row_lo, row_hi = 0, n
+    if args.scaling == "strong" and world > 1:
+        # flops-balanced 1-D row blocks of the left operand
+        h, a = P.host(), A.host()
+        blen = np.diff(a.row_ptr.astype(np.int64))
+        flops_row = np.add.reduceat(np.concatenate([blen[h.col_idx], [0]]),
+                                    np.minimum(h.row_ptr[:-1].astype(np.int64), len(h.col_idx)))
+        flops_row[np.diff(h.row_ptr.astype(np.int64)) == 0] = 0
+        cum = np.cumsum(flops_row)
+        cuts = [0] + [int(np.searchsorted(cum, cum[-1] * r / world)) for r in range(1, world)] + [n]
+        row_lo, row_hi = cuts[rank], cuts[rank + 1]
+
+    flags = slat.FLAG_TIMING
+
+    def step():
+        C = P.matmul_rowblock(row_lo, row_hi, A, flags)
+        nz = C.nnz()
+        del C
+        return nz
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        ctx.sync()
+
+    barrier()
+    sym, scan, num, tot = [], [], [], []
+    t0 = time.perf_counter()
+    nnz_c = 0
+    for _ in range(args.steps):
+        nnz_c = step()
+        st = ctx.stats()
+        sym.append(st["symbolic_ms"]), scan.append(st["scan_ms"]), num.append(st["numeric_ms"])
+        tot.append(st["total_ms"])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stats = ctx.stats()
+
+    units = nnz_c * args.steps
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        u = torch.tensor([units], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        units = int(u.item())
+
+    value = units / elapsed / 1e9
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        nnz_a = P.nnz() if row_hi - row_lo == n else int(P.row_ptr[row_hi] - P.row_ptr[row_lo])
+        alg = algorithmic_bytes(nnz_a, A.nnz(), nnz_c, row_hi - row_lo, 4)
+        num_ms = float(np.mean(num))
+        achieved = alg / (num_ms * 1e-3) / 1e9
+        pmc = load_pmc(f"torus{side}_a{power}")
+        traffic = pmc.get("numeric_bytes_per_launch") if pmc else None
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "kernel": "k_numeric", "algorithmic_bytes": alg,
+                    "kernel_ms": {"symbolic": round(float(np.mean(sym)), 4), "scan": round(float(np.mean(scan)), 4),
+                                  "numeric": round(num_ms, 4), "device_total": round(float(np.mean(tot)), 4)},
+                    "pipeline_frac": round(alg / (float(np.mean(tot)) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+        cpu = None
+        if not args.no_cpu and world == 1:
+            cpu = cpu_baseline(side, power, args.cpu_seconds)
+        workload = f"{side}^3 Moore torus thinned to 3 e/n (seed [42;32]), C = A^{power - 1} * A, u32 saturating"
+        out = {
+            "metric": "GNNZ/s (output nnz/s) for A×A on 30³ Moore torus, 1/2/4/8 GPUs",
+            "value": round(value, 4), "unit": "GNNZ/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak" if args.scaling == "weak" else "strong",
+            "vs_baseline": round(value / README_CSR_PAR_A7_GNNZ, 2) if (side, power) == (30, 7) else None,
+            "dtype": "u32", "data": "synthetic (reference generator: ChaCha12 StdRng seed [42;32])",
+            "config": {"workload": workload, "nnz_c": nnz_c, "n": n, "rows": [row_lo, row_hi],
+                       "partition": "block-diagonal, one torus per rank" if args.scaling == "weak" else "flops-balanced row blocks",
+                       "capacity": stats["capacity"], "mode": stats["mode"], "window_words": stats["window_words"]},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+/*
+ * slat.h — C ABI of the MI355X-native SpGEMM engine (libslat.so, gfx950).
+ *
+ * Drop-in boundary for the reference's SpGEMM path (imlvts/sparse-linear-algebra-tests):
+ *
+ *   reference (Rust)                                          replaced by
+ *   CsrMatrix::matmul       src/graph_csr.rs:306-346         slat_spgemm_csr_u32 (flags 0)
+ *   CsrMatrix::matmul_par   src/graph_csr.rs:350-484         slat_spgemm_csr_u32 (same result)
+ *   MagnusMatrix::matmul    src/graph_magnus.rs:224-232      slat_spgemm_csr_sat64
+ *   MagnusMatrix::matmul_seq src/graph_magnus.rs:234-242     slat_spgemm_csr_sat64
+ *   linalg Csr<u32,f64>::matmul{,_par} linalg/src/csr.rs:308-466  slat_spgemm_csr_f64
+ *   assert_eq!(self.n, other.n) panics (graph_csr.rs:307,351)  -> SLAT_EDIM
+ *
+ * Conventions:
+ *   * Inputs are borrowed read-only views (`&self`, `&Self`); device- or host-resident.
+ *   * The output is a freshly allocated, library-owned device matrix; release it with
+ *     slat_csr_free. Nothing is cached across calls except scratch in the context.
+ *   * Layout = the reference's: row_ptr u64 (usize) [n_rows+1], col_idx u32 (NodeId) sorted and
+ *     unique within a row, values u32 (saturating) | u64 (Sat64, saturating) | f64; no explicit
+ *     zeros in outputs. MagnusMatrix's usize column indices are narrowed to u32 (n < 2^32).
+ *   * Results equal CsrMatrix::matmul bit for bit (u32 / Sat64; order-independent because values
+ *     are non-negative) and the linalg f64 left fold in A-row order bit for bit (f64).
+ *   * One slat_ctx per host thread / stream. Calls are synchronous on the context's stream.
+ */
+#ifndef SLAT_H
+#define SLAT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SLAT_OK = 0,
+    SLAT_EINVAL = 1,   /* bad argument / malformed CSR / dtype mismatch */
+    SLAT_EDIM = 2,     /* shape mismatch (the reference panics: assert_eq!(self.n, other.n)) */
+    SLAT_EOOM = 3,     /* device or host allocation failed */
+    SLAT_EHIP = 4,     /* HIP runtime error */
+    SLAT_ENOTSUP = 5,  /* unsupported combination */
+    SLAT_ENODEV = 6    /* no usable gfx950 device */
+} slat_status;
+
+typedef enum { SLAT_U32 = 0, SLAT_SAT64 = 1, SLAT_F64 = 2 } slat_dtype;
+
+typedef enum { SLAT_DEVICE = 0, SLAT_HOST = 1 } slat_residency;
+
+/* spgemm flags */
+#define SLAT_FLAG_TIMING      0x1u  /* record per-kernel HIP events; read with slat_get_stats */
+#define SLAT_FLAG_EXACT_ALLOC 0x2u  /* size C exactly (extra mid-call sync) instead of by bound */
+#define SLAT_FLAG_STATS       0x4u  /* also count scalar products (flops) for slat_get_stats */
+
+typedef struct slat_ctx slat_ctx;
+
+/* Borrowed CSR view. row_ptr holds absolute offsets into col_idx/values (a row block of a larger
+ * matrix is a view with row_ptr advanced, n_rows reduced). max_row_nnz = 0 means unknown. */
+typedef struct {
+    uint64_t n_rows, n_cols, nnz;
+    const uint64_t *row_ptr;
+    const uint32_t *col_idx;
+    const void *values;
+    int32_t dtype;      /* slat_dtype */
+    int32_t residency;  /* slat_residency */
+    uint64_t max_row_nnz;
+} slat_csr_view;
+
+/* Library-owned device CSR. capacity >= nnz entries are allocated for col_idx/values. */
+typedef struct {
+    uint64_t n_rows, n_cols, nnz, capacity, max_row_nnz;
+    uint64_t *row_ptr;
+    uint32_t *col_idx;
+    void *values;
+    int32_t dtype;
+    int32_t device;
+} slat_csr;
+
+typedef struct {
+    uint64_t nnz;          /* nnz(C) of the last call */
+    uint64_t flops;        /* scalar products (only with SLAT_FLAG_STATS) */
+    uint64_t capacity;     /* entries allocated for C */
+    double symbolic_ms;    /* kernel durations (only with SLAT_FLAG_TIMING) */
+    double scan_ms;
+    double numeric_ms;
+    double compact_ms;
+    double total_ms;       /* first event to last event on the stream */
+    uint32_t mode;         /* traversal mode used (0 lane-per-A-entry, 1 wave-per-A-entry) */
+    uint32_t window_words; /* LDS bitmap words per window */
+    uint32_t exact_alloc;  /* 1 if the mid-call-sync path was taken */
+    uint32_t dropped_rows; /* rows that lost explicit zeros in the numeric pass */
+} slat_stats;
+
+/* --- context ------------------------------------------------------------------------------ */
+slat_status slat_ctx_create(int device, slat_ctx **out);
+slat_status slat_ctx_destroy(slat_ctx *ctx);
+slat_status slat_ctx_set_stream(slat_ctx *ctx, void *hip_stream); /* NULL = the ctx's own stream */
+void *slat_ctx_stream(slat_ctx *ctx);
+const char *slat_status_string(slat_status s);
+const char *slat_last_error(slat_ctx *ctx);
+slat_status slat_get_stats(slat_ctx *ctx, slat_stats *out);
+slat_status slat_sync(slat_ctx *ctx);
+
+/* --- matrices ----------------------------------------------------------------------------- */
+slat_status slat_csr_create(slat_ctx *ctx, const slat_csr_view *src, slat_csr *out); /* copy H2D/D2D */
+slat_status slat_csr_to_host(slat_ctx *ctx, const slat_csr_view *src, uint64_t *row_ptr,
+                             uint32_t *col_idx, void *values);
+slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m);
+slat_csr_view slat_csr_view_of(const slat_csr *m);
+slat_status slat_csr_max_row_nnz(slat_ctx *ctx, const slat_csr_view *m, uint64_t *out);
+
+/* --- SpGEMM: C = A * B ---------------------------------------------------------------------- */
+slat_status slat_spgemm(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, slat_csr *C,
+                        uint32_t flags);
+slat_status slat_spgemm_csr_u32(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B,
+                                slat_csr *C, uint32_t flags);
+slat_status slat_spgemm_csr_sat64(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B,
+                                  slat_csr *C, uint32_t flags);
+slat_status slat_spgemm_csr_f64(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B,
+                                slat_csr *C, uint32_t flags);
+/* Rows [row_begin, row_end) of A times B -> C with (row_end - row_begin) local rows: the 1-D
+ * row-block partition used across GPUs. */
+slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
+                                 uint64_t row_end, const slat_csr_view *B, slat_csr *C, uint32_t flags);
+
+/* --- host-side input generators (the reference's constructors) ------------------------------ */
+/* Host CSR owned by the library (malloc); free with slat_host_csr_free. */
+typedef struct {
+    uint64_t n, nnz;
+    uint64_t *row_ptr;
+    uint32_t *col_idx;
+    void *values;
+    int32_t dtype;
+    int32_t _pad;
+} slat_host_csr;
+
+typedef struct { uint8_t opaque[512]; } slat_rng; /* rand 0.9 StdRng (ChaCha12) state */
+
+void slat_rng_seed(slat_rng *rng, const uint8_t seed[32]);
+uint64_t slat_rng_next_u64(slat_rng *rng);
+double slat_rng_next_f64(slat_rng *rng);
+/* CsrMatrix::from_coo (src/graph_csr.rs:83-129): sort, merge duplicates by summing, drop zeros. */
+slat_status slat_host_from_coo(uint64_t n, uint64_t ntrip, const uint32_t *rows, const uint32_t *cols,
+                               const void *vals, int32_t dtype, slat_host_csr *out);
+/* CsrMatrix::lattice (src/graph_csr.rs:177-222). */
+slat_status slat_host_lattice(const uint64_t *dims, int ndim, int torus, slat_host_csr *out);
+/* CsrMatrix::thin (src/graph_csr.rs:225-247). */
+slat_status slat_host_thin(const slat_host_csr *m, slat_rng *rng, double density, slat_host_csr *out);
+/* Seeded R-MAT power-law graph with f64 values uniform in [0.5, 1.5) (config C5; not in the
+ * reference, which has no power-law generator). */
+slat_status slat_host_rmat(uint32_t scale, uint64_t n_edges, double a, double b, double c,
+                           const uint8_t seed[32], slat_host_csr *out);
+void slat_host_csr_free(slat_host_csr *m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLAT_H */

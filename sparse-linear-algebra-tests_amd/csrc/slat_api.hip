@@ -1,0 +1,559 @@
+// slat_api.hip — C ABI (include/slat.h) over the gfx950 SpGEMM kernels.
+//
+// Orchestration of one C = A·B call on the context's stream:
+//   1. C.row_ptr and C.col/val allocated from the stream-ordered pool (hipMallocAsync). By
+//      default C is sized by the exact upper bound nnz(A)·max_row_nnz(B) (clamped to rows·cols),
+//      so no host round trip is needed between the symbolic and numeric passes; the capacity is
+//      recorded in slat_csr.capacity. SLAT_FLAG_EXACT_ALLOC (or a bound above the memory budget)
+//      takes the reference's exact-size path instead: sync after the scan, allocate nnz(C).
+//   2. k_symbolic -> hipcub::DeviceScan::InclusiveSum -> k_numeric, all stream-ordered.
+//   3. One D2H of the 64 status shards (nnz, max row nnz, dropped-zero rows) + stream sync.
+//   4. Rare: k_compact when explicit zeros were dropped.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "slat.h"
+#include "spgemm_kernels.hpp"
+
+using namespace slat;
+
+struct slat_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int cu_count = 256;
+    size_t lds_per_block_max = 65536;
+    // workspace (grown on demand)
+    void *ws = nullptr;
+    size_t ws_bytes = 0;
+    unsigned long long *h_shards = nullptr;  // pinned
+    hipEvent_t ev[6] = {};
+    slat_stats stats = {};
+};
+
+#define SLAT_HIP(ctx, expr)                                                                        \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                        \
+            return SLAT_EHIP;                                                                      \
+        }                                                                                          \
+    } while (0)
+
+static slat_status fail(slat_ctx *ctx, slat_status s, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return s;
+}
+
+static size_t vsize(int32_t dtype) { return dtype == SLAT_U32 ? 4 : 8; }
+
+extern "C" {
+
+const char *slat_status_string(slat_status s) {
+    switch (s) {
+    case SLAT_OK: return "ok";
+    case SLAT_EINVAL: return "invalid argument";
+    case SLAT_EDIM: return "dimension mismatch";
+    case SLAT_EOOM: return "out of memory";
+    case SLAT_EHIP: return "HIP error";
+    case SLAT_ENOTSUP: return "not supported";
+    case SLAT_ENODEV: return "no gfx950 device";
+    }
+    return "unknown";
+}
+
+const char *slat_last_error(slat_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+slat_status slat_ctx_create(int device, slat_ctx **out) {
+    if (!out) return SLAT_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return SLAT_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SLAT_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SLAT_ENODEV;
+    slat_ctx *ctx = new slat_ctx();
+    ctx->device = device;
+    ctx->cu_count = prop.multiProcessorCount;
+    ctx->lds_per_block_max = prop.sharedMemPerBlock;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return SLAT_EHIP;
+    }
+    ctx->stream = ctx->own_stream;
+    // keep freed pool memory cached: C arrays are allocated every call
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    if (hipHostMalloc((void **)&ctx->h_shards, sizeof(unsigned long long) * kShards * kShardStride) != hipSuccess) {
+        (void)hipStreamDestroy(ctx->own_stream);
+        delete ctx;
+        return SLAT_EOOM;
+    }
+    for (auto &e : ctx->ev) (void)hipEventCreate(&e);
+    *out = ctx;
+    return SLAT_OK;
+}
+
+slat_status slat_ctx_destroy(slat_ctx *ctx) {
+    if (!ctx) return SLAT_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->h_shards) (void)hipHostFree(ctx->h_shards);
+    for (auto &e : ctx->ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return SLAT_OK;
+}
+
+slat_status slat_ctx_set_stream(slat_ctx *ctx, void *s) {
+    if (!ctx) return SLAT_EINVAL;
+    ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    return SLAT_OK;
+}
+
+void *slat_ctx_stream(slat_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+slat_status slat_sync(slat_ctx *ctx) {
+    if (!ctx) return SLAT_EINVAL;
+    SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SLAT_OK;
+}
+
+slat_status slat_get_stats(slat_ctx *ctx, slat_stats *out) {
+    if (!ctx || !out) return SLAT_EINVAL;
+    *out = ctx->stats;
+    return SLAT_OK;
+}
+
+slat_csr_view slat_csr_view_of(const slat_csr *m) {
+    slat_csr_view v;
+    std::memset(&v, 0, sizeof v);
+    if (!m) return v;
+    v.n_rows = m->n_rows;
+    v.n_cols = m->n_cols;
+    v.nnz = m->nnz;
+    v.row_ptr = m->row_ptr;
+    v.col_idx = m->col_idx;
+    v.values = m->values;
+    v.dtype = m->dtype;
+    v.residency = SLAT_DEVICE;
+    v.max_row_nnz = m->max_row_nnz;
+    return v;
+}
+
+slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m) {
+    if (!ctx || !m) return SLAT_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    if (m->row_ptr) (void)hipFreeAsync(m->row_ptr, ctx->stream);
+    if (m->col_idx) (void)hipFreeAsync(m->col_idx, ctx->stream);
+    if (m->values) (void)hipFreeAsync(m->values, ctx->stream);
+    std::memset(m, 0, sizeof *m);
+    return SLAT_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+static slat_status ensure_ws(slat_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->ws_bytes) return SLAT_OK;
+    SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->ws) SLAT_HIP(ctx, hipFree(ctx->ws));
+    ctx->ws = nullptr;
+    ctx->ws_bytes = 0;
+    size_t nb = std::max(bytes, (size_t)1 << 20);
+    nb = std::max(nb, ctx->ws_bytes * 2);
+    if (hipMalloc(&ctx->ws, nb) != hipSuccess) return fail(ctx, SLAT_EOOM, "workspace allocation failed");
+    ctx->ws_bytes = nb;
+    return SLAT_OK;
+}
+
+static slat_status check_view(slat_ctx *ctx, const slat_csr_view *v, const char *name) {
+    if (!v) return fail(ctx, SLAT_EINVAL, std::string(name) + " is null");
+    if (v->dtype < SLAT_U32 || v->dtype > SLAT_F64) return fail(ctx, SLAT_EINVAL, std::string(name) + ": bad dtype");
+    if (v->n_rows && !v->row_ptr) return fail(ctx, SLAT_EINVAL, std::string(name) + ": null row_ptr");
+    if (v->nnz && (!v->col_idx || !v->values)) return fail(ctx, SLAT_EINVAL, std::string(name) + ": null arrays");
+    if (v->n_cols > 0xFFFFFFFFull || v->n_rows > 0xFFFFFFFFull) return fail(ctx, SLAT_EINVAL, std::string(name) + ": dims exceed u32 ids");
+    return SLAT_OK;
+}
+
+extern "C" slat_status slat_csr_create(slat_ctx *ctx, const slat_csr_view *src, slat_csr *out) {
+    if (!ctx || !out) return SLAT_EINVAL;
+    slat_status st = check_view(ctx, src, "src");
+    if (st) return st;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    std::memset(out, 0, sizeof *out);
+    const size_t vs = vsize(src->dtype);
+    const hipMemcpyKind kind = src->residency == SLAT_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    SLAT_HIP(ctx, hipMallocAsync((void **)&out->row_ptr, (src->n_rows + 1) * 8, ctx->stream));
+    SLAT_HIP(ctx, hipMallocAsync((void **)&out->col_idx, std::max<uint64_t>(src->nnz, 1) * 4, ctx->stream));
+    SLAT_HIP(ctx, hipMallocAsync(&out->values, std::max<uint64_t>(src->nnz, 1) * vs, ctx->stream));
+    if (src->n_rows)
+        SLAT_HIP(ctx, hipMemcpyAsync(out->row_ptr, src->row_ptr, (src->n_rows + 1) * 8, kind, ctx->stream));
+    else
+        SLAT_HIP(ctx, hipMemsetAsync(out->row_ptr, 0, 8, ctx->stream));
+    if (src->nnz) {
+        SLAT_HIP(ctx, hipMemcpyAsync(out->col_idx, src->col_idx, src->nnz * 4, kind, ctx->stream));
+        SLAT_HIP(ctx, hipMemcpyAsync(out->values, src->values, src->nnz * vs, kind, ctx->stream));
+    }
+    out->n_rows = src->n_rows;
+    out->n_cols = src->n_cols;
+    out->nnz = src->nnz;
+    out->capacity = src->nnz;
+    out->dtype = src->dtype;
+    out->device = ctx->device;
+    uint64_t mr = src->max_row_nnz;
+    if (mr == 0 && src->n_rows) {
+        if (src->residency == SLAT_HOST) {
+            for (uint64_t i = 0; i < src->n_rows; ++i) mr = std::max(mr, src->row_ptr[i + 1] - src->row_ptr[i]);
+        } else {
+            slat_csr_view v = slat_csr_view_of(out);
+            st = slat_csr_max_row_nnz(ctx, &v, &mr);
+            if (st) return st;
+        }
+    }
+    out->max_row_nnz = mr;
+    SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SLAT_OK;
+}
+
+extern "C" slat_status slat_csr_to_host(slat_ctx *ctx, const slat_csr_view *src, uint64_t *row_ptr, uint32_t *col,
+                                        void *vals) {
+    if (!ctx) return SLAT_EINVAL;
+    slat_status st = check_view(ctx, src, "src");
+    if (st) return st;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    const hipMemcpyKind kind = src->residency == SLAT_HOST ? hipMemcpyHostToHost : hipMemcpyDeviceToHost;
+    if (row_ptr) SLAT_HIP(ctx, hipMemcpyAsync(row_ptr, src->row_ptr, (src->n_rows + 1) * 8, kind, ctx->stream));
+    if (src->nnz && col) SLAT_HIP(ctx, hipMemcpyAsync(col, src->col_idx, src->nnz * 4, kind, ctx->stream));
+    if (src->nnz && vals) SLAT_HIP(ctx, hipMemcpyAsync(vals, src->values, src->nnz * vsize(src->dtype), kind, ctx->stream));
+    SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SLAT_OK;
+}
+
+extern "C" slat_status slat_csr_max_row_nnz(slat_ctx *ctx, const slat_csr_view *m, uint64_t *out) {
+    if (!ctx || !m || !out) return SLAT_EINVAL;
+    *out = 0;
+    if (m->n_rows == 0) return SLAT_OK;
+    if (m->residency == SLAT_HOST) {
+        uint64_t mr = 0;
+        for (uint64_t i = 0; i < m->n_rows; ++i) mr = std::max(mr, m->row_ptr[i + 1] - m->row_ptr[i]);
+        *out = mr;
+        return SLAT_OK;
+    }
+    slat_status st = ensure_ws(ctx, 4096);
+    if (st) return st;
+    unsigned long long *shards = (unsigned long long *)ctx->ws;
+    SLAT_HIP(ctx, hipMemsetAsync(shards, 0, sizeof(unsigned long long) * kShards * kShardStride, ctx->stream));
+    const uint64_t blocks = std::min<uint64_t>((m->n_rows + kBlock - 1) / kBlock, 1024);
+    hipLaunchKernelGGL(k_max_row, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream, m->row_ptr, m->n_rows, shards);
+    SLAT_HIP(ctx, hipGetLastError());
+    SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, shards, sizeof(unsigned long long) * kShards * kShardStride,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t mr = 0;
+    for (int s = 0; s < kShards; ++s) mr = std::max<uint64_t>(mr, ctx->h_shards[s * kShardStride + 1]);
+    *out = mr;
+    return SLAT_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// launch helpers (templated over semiring and traversal modes)
+// ---------------------------------------------------------------------------------------------
+template <typename Sem>
+static hipError_t launch_numeric(uint32_t build_mode, uint32_t acc_mode, dim3 grid, size_t lds, hipStream_t s,
+                                 const Args &a) {
+    if constexpr (Sem::kOrdered) {
+        if (build_mode == MODE_LANE_PER_A)
+            hipLaunchKernelGGL((k_numeric<Sem, MODE_LANE_PER_A, MODE_WAVE_PER_A>), grid, dim3(kBlock), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_numeric<Sem, MODE_WAVE_PER_A, MODE_WAVE_PER_A>), grid, dim3(kBlock), lds, s, a);
+    } else {
+        (void)acc_mode;
+        if (build_mode == MODE_LANE_PER_A)
+            hipLaunchKernelGGL((k_numeric<Sem, MODE_LANE_PER_A, MODE_LANE_PER_A>), grid, dim3(kBlock), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_numeric<Sem, MODE_WAVE_PER_A, MODE_WAVE_PER_A>), grid, dim3(kBlock), lds, s, a);
+    }
+    return hipGetLastError();
+}
+
+template <typename S>
+static hipError_t launch_compact(dim3 grid, hipStream_t s, const uint64_t *orp, const uint64_t *nrp, uint64_t n,
+                                 const uint32_t *oc, const void *ov, uint32_t *nc, void *nv) {
+    hipLaunchKernelGGL(k_compact<S>, grid, dim3(kBlock), 0, s, orp, nrp, n, oc, (const S *)ov, nc, (S *)nv);
+    return hipGetLastError();
+}
+
+static size_t scan_temp_bytes(uint64_t n) {
+    size_t tb = 0;
+    hipcub::DeviceScan::InclusiveSum(nullptr, tb, (const uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
+    return (tb + 255) & ~(size_t)255;
+}
+
+// Window geometry: ww = 64 * per with `per` odd (lane-contiguous word ownership is then free of
+// LDS bank conflicts). One window covers all columns when n_cols <= 64·31·32.
+static void pick_window(uint64_t ncols, uint32_t &ww, uint32_t &wide) {
+    const uint64_t words = (ncols + 31) / 32;
+    uint64_t per = (words + kWave - 1) / kWave;
+    if (per == 0) per = 1;
+    if (per <= 31) {
+        if ((per & 1) == 0) per += 1;
+        wide = 0;
+    } else {
+        per = 31;
+        wide = 1;
+    }
+    ww = (uint32_t)(per * kWave);
+}
+
+extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
+                                            uint64_t row_end, const slat_csr_view *B, slat_csr *C, uint32_t flags) {
+    if (!ctx || !C) return SLAT_EINVAL;
+    slat_status st;
+    if ((st = check_view(ctx, A, "A")) || (st = check_view(ctx, B, "B"))) return st;
+    if (A->dtype != B->dtype) return fail(ctx, SLAT_EINVAL, "A and B value types differ");
+    if (A->n_cols != B->n_rows) return fail(ctx, SLAT_EDIM, "A.n_cols != B.n_rows");
+    if (row_begin > row_end || row_end > A->n_rows) return fail(ctx, SLAT_EINVAL, "bad row block");
+    if (A->residency != SLAT_DEVICE || B->residency != SLAT_DEVICE) {
+        // host inputs: stage through owned device copies (PCIe outside the engine's hot path)
+        slat_csr dA = {}, dB = {};
+        const slat_csr_view *pa = A, *pb = B;
+        slat_csr_view va, vb;
+        if (A->residency != SLAT_DEVICE) {
+            if ((st = slat_csr_create(ctx, A, &dA))) return st;
+            va = slat_csr_view_of(&dA);
+            pa = &va;
+        }
+        if (B->residency != SLAT_DEVICE) {
+            if ((st = slat_csr_create(ctx, B, &dB))) {
+                slat_csr_free(ctx, &dA);
+                return st;
+            }
+            vb = slat_csr_view_of(&dB);
+            pb = &vb;
+        }
+        st = slat_spgemm_rowblock(ctx, pa, row_begin, row_end, pb, C, flags);
+        if (dA.row_ptr) slat_csr_free(ctx, &dA);
+        if (dB.row_ptr) slat_csr_free(ctx, &dB);
+        return st;
+    }
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    std::memset(C, 0, sizeof *C);
+    std::memset(&ctx->stats, 0, sizeof ctx->stats);
+    const uint64_t n = row_end - row_begin;
+    const uint64_t ncols = B->n_cols;
+    const int32_t dt = A->dtype;
+    const size_t vs = vsize(dt);
+    hipStream_t s = ctx->stream;
+    C->n_rows = n;
+    C->n_cols = ncols;
+    C->dtype = dt;
+    C->device = ctx->device;
+    SLAT_HIP(ctx, hipMallocAsync((void **)&C->row_ptr, (n + 1) * 8, s));
+    if (n == 0 || ncols == 0 || A->nnz == 0 || B->nnz == 0) {
+        // empty product: all-zero row_ptr
+        SLAT_HIP(ctx, hipMemsetAsync(C->row_ptr, 0, (n + 1) * 8, s));
+        SLAT_HIP(ctx, hipMallocAsync((void **)&C->col_idx, 4, s));
+        SLAT_HIP(ctx, hipMallocAsync(&C->values, 8, s));
+        SLAT_HIP(ctx, hipStreamSynchronize(s));
+        return SLAT_OK;
+    }
+    uint64_t maxrow_b = B->max_row_nnz;
+    if (maxrow_b == 0 && (st = slat_csr_max_row_nnz(ctx, B, &maxrow_b))) return st;
+    const uint64_t a_nnz_block = A->nnz;  // upper bound for the block too
+
+    Args a = {};
+    a.a_rp = A->row_ptr + row_begin;
+    a.a_col = A->col_idx;
+    a.a_val = A->values;
+    a.b_rp = B->row_ptr;
+    a.b_col = B->col_idx;
+    a.b_val = B->values;
+    a.nrows = n;
+    a.ncols = ncols;
+    pick_window(ncols, a.ww, a.wide);
+    a.cap = 1024;
+    a.stats = (flags & SLAT_FLAG_STATS) ? 1u : 0u;
+
+    const uint32_t build_mode = maxrow_b <= 32 ? MODE_LANE_PER_A : MODE_WAVE_PER_A;
+    const uint32_t acc_mode = dt == SLAT_F64 ? MODE_WAVE_PER_A : build_mode;
+
+    // workspace: counts [n] | shards | scan temp
+    const size_t counts_b = ((n * 8) + 255) & ~(size_t)255;
+    const size_t shards_b = 4096;
+    const size_t scan_b = scan_temp_bytes(n);
+    if ((st = ensure_ws(ctx, counts_b + shards_b + scan_b + 2 * (((n + 1) * 8 + 255) & ~(size_t)255)))) return st;
+    uint8_t *ws = (uint8_t *)ctx->ws;
+    a.counts = (uint64_t *)ws;
+    a.shards = (unsigned long long *)(ws + counts_b);
+    void *scan_tmp = ws + counts_b + shards_b;
+    size_t scan_tb = scan_b;
+    a.c_rp = C->row_ptr;
+
+    // capacity by exact bound (no mid-call sync) unless it exceeds the budget
+    unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
+    const unsigned __int128 dense = (unsigned __int128)n * ncols;
+    if (bound128 > dense) bound128 = dense;
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    const unsigned __int128 budget = (unsigned __int128)free_b / 4;
+    const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
+    if (!exact) {
+        C->capacity = (uint64_t)std::max<unsigned __int128>(bound128, 1);
+        SLAT_HIP(ctx, hipMallocAsync((void **)&C->col_idx, C->capacity * 4, s));
+        SLAT_HIP(ctx, hipMallocAsync(&C->values, C->capacity * vs, s));
+    }
+
+    // LDS sizing and grid
+    const size_t sym_lds = (size_t)kWavesPerBlock * a.ww * 4;
+    size_t num_lds = (size_t)kWavesPerBlock * numeric_wave_lds(a.ww, a.cap);
+    while (num_lds > ctx->lds_per_block_max && a.cap > 64) {
+        a.cap /= 2;
+        num_lds = (size_t)kWavesPerBlock * numeric_wave_lds(a.ww, a.cap);
+    }
+    const uint64_t want_blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint64_t max_blocks = (uint64_t)ctx->cu_count * 8;
+    const dim3 grid((unsigned)std::max<uint64_t>(1, std::min(want_blocks, max_blocks)));
+    const bool timing = flags & SLAT_FLAG_TIMING;
+
+    if (a.stats) SLAT_HIP(ctx, hipMemsetAsync(a.shards, 0, 4096, s));
+    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
+    if (build_mode == MODE_LANE_PER_A)
+        hipLaunchKernelGGL(k_symbolic<MODE_LANE_PER_A>, grid, dim3(kBlock), sym_lds, s, a);
+    else
+        hipLaunchKernelGGL(k_symbolic<MODE_WAVE_PER_A>, grid, dim3(kBlock), sym_lds, s, a);
+    SLAT_HIP(ctx, hipGetLastError());
+    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+    SLAT_HIP(ctx, hipcub::DeviceScan::InclusiveSum(scan_tmp, scan_tb, a.counts, C->row_ptr + 1, (int)n, s));
+    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+
+    if (exact) {
+        uint64_t total = 0;
+        SLAT_HIP(ctx, hipMemcpyAsync(&total, C->row_ptr + n, 8, hipMemcpyDeviceToHost, s));
+        SLAT_HIP(ctx, hipStreamSynchronize(s));
+        C->capacity = std::max<uint64_t>(total, 1);
+        if (hipMallocAsync((void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
+            hipMallocAsync(&C->values, C->capacity * vs, s) != hipSuccess) {
+            slat_csr_free(ctx, C);
+            return fail(ctx, SLAT_EOOM, "C allocation failed");
+        }
+        if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+    }
+    a.c_col = C->col_idx;
+    a.c_val = C->values;
+    hipError_t e;
+    if (dt == SLAT_U32)
+        e = launch_numeric<SemU32>(build_mode, acc_mode, grid, num_lds, s, a);
+    else if (dt == SLAT_SAT64)
+        e = launch_numeric<SemSat64>(build_mode, acc_mode, grid, num_lds, s, a);
+    else
+        e = launch_numeric<SemF64>(build_mode, acc_mode, grid, num_lds, s, a);
+    SLAT_HIP(ctx, e);
+    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
+    SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
+                                 hipMemcpyDeviceToHost, s));
+    SLAT_HIP(ctx, hipStreamSynchronize(s));
+
+    uint64_t nnz = ctx->h_shards[0], maxrow = 0, drops = 0, flops = 0;
+    for (int i = 0; i < kShards; ++i) {
+        maxrow = std::max<uint64_t>(maxrow, ctx->h_shards[i * kShardStride + 1]);
+        drops += ctx->h_shards[i * kShardStride + 2];
+        flops += ctx->h_shards[i * kShardStride + 3];
+    }
+    double compact_ms = 0;
+    if (drops) {
+        // exact zeros were dropped: rebuild row_ptr from the per-row actual counts and move rows
+        uint64_t *nrp = nullptr;
+        SLAT_HIP(ctx, hipMallocAsync((void **)&nrp, (n + 1) * 8, s));
+        SLAT_HIP(ctx, hipMemsetAsync(nrp, 0, 8, s));
+        SLAT_HIP(ctx, hipcub::DeviceScan::InclusiveSum(scan_tmp, scan_tb, a.counts, nrp + 1, (int)n, s));
+        uint64_t total = 0;
+        SLAT_HIP(ctx, hipMemcpyAsync(&total, nrp + n, 8, hipMemcpyDeviceToHost, s));
+        SLAT_HIP(ctx, hipStreamSynchronize(s));
+        uint32_t *ncol = nullptr;
+        void *nval = nullptr;
+        SLAT_HIP(ctx, hipMallocAsync((void **)&ncol, std::max<uint64_t>(total, 1) * 4, s));
+        SLAT_HIP(ctx, hipMallocAsync(&nval, std::max<uint64_t>(total, 1) * vs, s));
+        if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
+        if (vs == 4)
+            e = launch_compact<uint32_t>(grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
+        else
+            e = launch_compact<uint64_t>(grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
+        SLAT_HIP(ctx, e);
+        if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
+        (void)hipFreeAsync(C->row_ptr, s);
+        (void)hipFreeAsync(C->col_idx, s);
+        (void)hipFreeAsync(C->values, s);
+        SLAT_HIP(ctx, hipStreamSynchronize(s));
+        C->row_ptr = nrp;
+        C->col_idx = ncol;
+        C->values = nval;
+        C->capacity = std::max<uint64_t>(total, 1);
+        nnz = total;
+        if (timing) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, ctx->ev[4], ctx->ev[5]);
+            compact_ms = ms;
+        }
+    }
+    C->nnz = nnz;
+    C->max_row_nnz = maxrow;
+
+    slat_stats &S = ctx->stats;
+    S.nnz = nnz;
+    S.flops = flops;
+    S.capacity = C->capacity;
+    S.mode = build_mode;
+    S.window_words = a.ww;
+    S.exact_alloc = exact ? 1u : 0u;
+    S.dropped_rows = (uint32_t)drops;
+    if (timing) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        S.symbolic_ms = ms;
+        (void)hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]);
+        S.scan_ms = ms;
+        (void)hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]);
+        S.numeric_ms = ms;
+        S.compact_ms = compact_ms;
+        (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]);
+        S.total_ms = ms + compact_ms;
+    }
+    return SLAT_OK;
+}
+
+extern "C" slat_status slat_spgemm(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, slat_csr *C,
+                                   uint32_t flags) {
+    if (!ctx || !A) return SLAT_EINVAL;
+    return slat_spgemm_rowblock(ctx, A, 0, A->n_rows, B, C, flags);
+}
+
+static slat_status typed(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, slat_csr *C, uint32_t flags,
+                         int32_t dt) {
+    if (!ctx || !A || !B) return SLAT_EINVAL;
+    if (A->dtype != dt || B->dtype != dt) return fail(ctx, SLAT_EINVAL, "value type does not match the entry point");
+    return slat_spgemm(ctx, A, B, C, flags);
+}
+
+extern "C" slat_status slat_spgemm_csr_u32(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, slat_csr *C,
+                                           uint32_t flags) {
+    return typed(ctx, A, B, C, flags, SLAT_U32);
+}
+extern "C" slat_status slat_spgemm_csr_sat64(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B,
+                                             slat_csr *C, uint32_t flags) {
+    return typed(ctx, A, B, C, flags, SLAT_SAT64);
+}
+extern "C" slat_status slat_spgemm_csr_f64(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, slat_csr *C,
+                                           uint32_t flags) {
+    return typed(ctx, A, B, C, flags, SLAT_F64);
+}

@@ -1,0 +1,126 @@
+"""ctypes binding of libslat.so (include/slat.h). The HIP engine is the only compute path: if the
+library cannot be loaded, importing the GPU entry points raises — there is no CPU fallback."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libslat.so")
+
+SLAT_OK, SLAT_EINVAL, SLAT_EDIM, SLAT_EOOM, SLAT_EHIP, SLAT_ENOTSUP, SLAT_ENODEV = range(7)
+U32, SAT64, F64 = 0, 1, 2
+DEVICE, HOST = 0, 1
+FLAG_TIMING, FLAG_EXACT_ALLOC, FLAG_STATS = 0x1, 0x2, 0x4
+
+# Every symbol include/slat.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "slat_ctx_create", "slat_ctx_destroy", "slat_ctx_set_stream", "slat_ctx_stream", "slat_status_string",
+    "slat_last_error", "slat_get_stats", "slat_sync", "slat_csr_create", "slat_csr_to_host", "slat_csr_free",
+    "slat_csr_view_of", "slat_csr_max_row_nnz", "slat_spgemm", "slat_spgemm_csr_u32", "slat_spgemm_csr_sat64",
+    "slat_spgemm_csr_f64", "slat_spgemm_rowblock", "slat_rng_seed", "slat_rng_next_u64", "slat_rng_next_f64",
+    "slat_host_from_coo", "slat_host_lattice", "slat_host_thin", "slat_host_rmat", "slat_host_csr_free",
+]
+
+
+class SlatError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"slat status {status}: {msg}")
+        self.status = status
+
+
+class CsrView(C.Structure):
+    _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_uint64), ("nnz", C.c_uint64), ("row_ptr", C.c_void_p),
+                ("col_idx", C.c_void_p), ("values", C.c_void_p), ("dtype", C.c_int32), ("residency", C.c_int32),
+                ("max_row_nnz", C.c_uint64)]
+
+
+class CsrOwned(C.Structure):
+    _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_uint64), ("nnz", C.c_uint64), ("capacity", C.c_uint64),
+                ("max_row_nnz", C.c_uint64), ("row_ptr", C.c_void_p), ("col_idx", C.c_void_p),
+                ("values", C.c_void_p), ("dtype", C.c_int32), ("device", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("nnz", C.c_uint64), ("flops", C.c_uint64), ("capacity", C.c_uint64), ("symbolic_ms", C.c_double),
+                ("scan_ms", C.c_double), ("numeric_ms", C.c_double), ("compact_ms", C.c_double),
+                ("total_ms", C.c_double), ("mode", C.c_uint32), ("window_words", C.c_uint32),
+                ("exact_alloc", C.c_uint32), ("dropped_rows", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class HostCsr(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("nnz", C.c_uint64), ("row_ptr", C.c_void_p), ("col_idx", C.c_void_p),
+                ("values", C.c_void_p), ("dtype", C.c_int32), ("_pad", C.c_int32)]
+
+
+class RngState(C.Structure):
+    _fields_ = [("opaque", C.c_uint8 * 512)]
+
+
+def build() -> str:
+    """Compile libslat.so in-tree (hipcc, gfx950)."""
+    subprocess.run(["make", "-s", "-C", PKG_DIR], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    """Load libslat.so (raises OSError if it has not been built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} not built; run `make -C {PKG_DIR}` or __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    P, vp, u64, i32, u32 = C.POINTER, C.c_void_p, C.c_uint64, C.c_int32, C.c_uint32
+    sig = {
+        "slat_ctx_create": ([C.c_int, P(vp)], C.c_int),
+        "slat_ctx_destroy": ([vp], C.c_int),
+        "slat_ctx_set_stream": ([vp, vp], C.c_int),
+        "slat_ctx_stream": ([vp], vp),
+        "slat_status_string": ([C.c_int], C.c_char_p),
+        "slat_last_error": ([vp], C.c_char_p),
+        "slat_get_stats": ([vp, P(Stats)], C.c_int),
+        "slat_sync": ([vp], C.c_int),
+        "slat_csr_create": ([vp, P(CsrView), P(CsrOwned)], C.c_int),
+        "slat_csr_to_host": ([vp, P(CsrView), vp, vp, vp], C.c_int),
+        "slat_csr_free": ([vp, P(CsrOwned)], C.c_int),
+        "slat_csr_view_of": ([P(CsrOwned)], CsrView),
+        "slat_csr_max_row_nnz": ([vp, P(CsrView), P(u64)], C.c_int),
+        "slat_spgemm": ([vp, P(CsrView), P(CsrView), P(CsrOwned), u32], C.c_int),
+        "slat_spgemm_csr_u32": ([vp, P(CsrView), P(CsrView), P(CsrOwned), u32], C.c_int),
+        "slat_spgemm_csr_sat64": ([vp, P(CsrView), P(CsrView), P(CsrOwned), u32], C.c_int),
+        "slat_spgemm_csr_f64": ([vp, P(CsrView), P(CsrView), P(CsrOwned), u32], C.c_int),
+        "slat_spgemm_rowblock": ([vp, P(CsrView), u64, u64, P(CsrView), P(CsrOwned), u32], C.c_int),
+        "slat_rng_seed": ([P(RngState), C.c_char_p], None),
+        "slat_rng_next_u64": ([P(RngState)], u64),
+        "slat_rng_next_f64": ([P(RngState)], C.c_double),
+        "slat_host_from_coo": ([u64, u64, vp, vp, vp, i32, P(HostCsr)], C.c_int),
+        "slat_host_lattice": ([P(u64), C.c_int, C.c_int, P(HostCsr)], C.c_int),
+        "slat_host_thin": ([P(HostCsr), P(RngState), C.c_double, P(HostCsr)], C.c_int),
+        "slat_host_rmat": ([u32, u64, C.c_double, C.c_double, C.c_double, C.c_char_p, P(HostCsr)], C.c_int),
+        "slat_host_csr_free": ([P(HostCsr)], None),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(status: int, ctx=None):
+    if status != SLAT_OK:
+        L = lib()
+        msg = L.slat_status_string(status).decode()
+        if ctx:
+            detail = L.slat_last_error(ctx)
+            if detail:
+                msg += f" ({detail.decode()})"
+        raise SlatError(status, msg)

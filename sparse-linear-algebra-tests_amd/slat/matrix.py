@@ -1,0 +1,383 @@
+"""Host-side mirror of the reference's matrix API, backed by the MI355X engine (libslat.so).
+
+  CsrMatrix    <- src/graph_csr.rs:42-53   (u32 ids, u32 saturating values)
+  MagnusMatrix <- src/graph_magnus.rs:11-14 (Sat64 values; usize cols narrowed to u32)
+  Csr          <- linalg/src/csr.rs:93-98  (value type u32 | u64 | f64)
+
+Matrices live in device memory (library-owned). `matmul` / `matmul_par` (CsrMatrix),
+`matmul` / `matmul_seq` (MagnusMatrix) all run the same HIP SpGEMM: the reference's seq/par
+variants differ only in CPU scheduling and produce identical results. Shape mismatches raise
+`SlatError(SLAT_EDIM)` where the reference panics on `assert_eq!(self.n, other.n)`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+_VDT = {L.U32: np.uint32, L.SAT64: np.uint64, L.F64: np.float64}
+_CT = {L.U32: C.c_uint32, L.SAT64: C.c_uint64, L.F64: C.c_double}
+
+
+class Context:
+    """One slat_ctx (device + stream). Not shared across host threads."""
+
+    def __init__(self, device: int = 0):
+        self._ptr = C.c_void_p()
+        L.check(L.lib().slat_ctx_create(device, C.byref(self._ptr)))
+        self.device = device
+
+    @property
+    def ptr(self):
+        return self._ptr
+
+    def close(self):
+        if self._ptr:
+            L.lib().slat_ctx_destroy(self._ptr)
+            self._ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stats(self) -> dict:
+        s = L.Stats()
+        L.check(L.lib().slat_get_stats(self._ptr, C.byref(s)), self._ptr)
+        return s.as_dict()
+
+    def set_stream(self, stream_ptr: int | None):
+        L.check(L.lib().slat_ctx_set_stream(self._ptr, C.c_void_p(stream_ptr or 0)), self._ptr)
+
+    def sync(self):
+        L.check(L.lib().slat_sync(self._ptr), self._ptr)
+
+
+_tls = threading.local()
+
+
+def default_context(device: int = 0) -> Context:
+    ctxs = getattr(_tls, "ctxs", None)
+    if ctxs is None:
+        ctxs = _tls.ctxs = {}
+    if device not in ctxs:
+        ctxs[device] = Context(device)
+    return ctxs[device]
+
+
+class StdRng:
+    """rand 0.9 `StdRng::from_seed` (ChaCha12), as used by the reference's benches."""
+
+    def __init__(self, seed: bytes = bytes([42] * 32)):
+        if len(seed) != 32:
+            raise ValueError("seed must be 32 bytes")
+        self._s = L.RngState()
+        L.lib().slat_rng_seed(C.byref(self._s), seed)
+
+    @classmethod
+    def from_seed(cls, seed) -> "StdRng":
+        return cls(bytes(seed))
+
+    def next_u64(self) -> int:
+        return int(L.lib().slat_rng_next_u64(C.byref(self._s)))
+
+    def random_f64(self) -> float:
+        return float(L.lib().slat_rng_next_f64(C.byref(self._s)))
+
+
+# ------------------------------------------------------------------------------------------------
+# host CSR (numpy) produced by the library's constructors
+# ------------------------------------------------------------------------------------------------
+class HostCsr:
+    """Plain host arrays: row_ptr u64 [n+1], col_idx u32, values."""
+
+    def __init__(self, n: int, row_ptr, col_idx, values, dtype: int):
+        self.n = int(n)
+        self.row_ptr = np.ascontiguousarray(row_ptr, np.uint64)
+        self.col_idx = np.ascontiguousarray(col_idx, np.uint32)
+        self.values = np.ascontiguousarray(values, _VDT[dtype])
+        self.dtype = dtype
+
+    @property
+    def nnz(self) -> int:
+        return int(len(self.col_idx))
+
+    @staticmethod
+    def _take(h: L.HostCsr) -> "HostCsr":
+        n, z, dt = int(h.n), int(h.nnz), int(h.dtype)
+        rp = np.ctypeslib.as_array(C.cast(h.row_ptr, C.POINTER(C.c_uint64)), (n + 1,)).copy()
+        if z:
+            col = np.ctypeslib.as_array(C.cast(h.col_idx, C.POINTER(C.c_uint32)), (z,)).copy()
+            val = np.ctypeslib.as_array(C.cast(h.values, C.POINTER(_CT[dt])), (z,)).copy()
+        else:
+            col, val = np.zeros(0, np.uint32), np.zeros(0, _VDT[dt])
+        L.lib().slat_host_csr_free(C.byref(h))
+        return HostCsr(n, rp, col, val, dt)
+
+    def _raw(self) -> L.HostCsr:
+        h = L.HostCsr()
+        h.n, h.nnz, h.dtype = self.n, self.nnz, self.dtype
+        h.row_ptr, h.col_idx, h.values = self.row_ptr.ctypes.data, self.col_idx.ctypes.data, self.values.ctypes.data
+        return h
+
+    def view(self) -> L.CsrView:
+        v = L.CsrView()
+        v.n_rows = v.n_cols = self.n
+        v.nnz = self.nnz
+        v.row_ptr, v.col_idx, v.values = self.row_ptr.ctypes.data, self.col_idx.ctypes.data, self.values.ctypes.data
+        v.dtype, v.residency = self.dtype, L.HOST
+        v.max_row_nnz = int(np.diff(self.row_ptr).max(initial=0))
+        return v
+
+    def astype(self, dtype: int) -> "HostCsr":
+        return HostCsr(self.n, self.row_ptr, self.col_idx, self.values.astype(_VDT[dtype]), dtype)
+
+
+def host_from_coo(n: int, rows, cols, vals, dtype: int = L.U32) -> HostCsr:
+    rows = np.ascontiguousarray(rows, np.uint32)
+    cols = np.ascontiguousarray(cols, np.uint32)
+    vals = np.ascontiguousarray(vals, _VDT[dtype])
+    h = L.HostCsr()
+    L.check(L.lib().slat_host_from_coo(n, len(rows), rows.ctypes.data, cols.ctypes.data, vals.ctypes.data, dtype,
+                                       C.byref(h)))
+    return HostCsr._take(h)
+
+
+def host_lattice(dims: Sequence[int], torus: bool) -> HostCsr:
+    d = (C.c_uint64 * len(dims))(*dims)
+    h = L.HostCsr()
+    L.check(L.lib().slat_host_lattice(d, len(dims), int(torus), C.byref(h)))
+    return HostCsr._take(h)
+
+
+def host_thin(m: HostCsr, rng: StdRng, density: float) -> HostCsr:
+    raw = m._raw()
+    h = L.HostCsr()
+    L.check(L.lib().slat_host_thin(C.byref(raw), C.byref(rng._s), float(density), C.byref(h)))
+    return HostCsr._take(h)
+
+
+def host_rmat(scale: int, n_edges: int, a=0.57, b=0.19, c=0.19, seed: bytes = bytes([42] * 32)) -> HostCsr:
+    h = L.HostCsr()
+    L.check(L.lib().slat_host_rmat(scale, n_edges, a, b, c, seed, C.byref(h)))
+    return HostCsr._take(h)
+
+
+def torus_thinned(side: int, epn: float, rng: StdRng) -> HostCsr:
+    """side^3 Moore torus thinned to `epn` edges per node (src/graph_magnus.rs:713-719)."""
+    full = host_lattice([side, side, side], True)
+    density = epn / (full.nnz / full.n)
+    return host_thin(full, rng, density) if density < 1.0 else full
+
+
+# ------------------------------------------------------------------------------------------------
+# device-resident matrices
+# ------------------------------------------------------------------------------------------------
+class DeviceCsr:
+    """A library-owned device CSR (slat_csr). Host arrays are fetched lazily."""
+
+    DTYPE = L.U32
+
+    def __init__(self, owned: L.CsrOwned, ctx: Context):
+        self._m = owned
+        self._ctx = ctx
+        self._host = None
+
+    def __del__(self):
+        try:
+            if self._m is not None and self._m.row_ptr:
+                L.lib().slat_csr_free(self._ctx.ptr, C.byref(self._m))
+        except Exception:
+            pass
+
+    # -- construction ----------------------------------------------------------------------------
+    @classmethod
+    def from_host(cls, h: HostCsr, ctx: Context | None = None):
+        ctx = ctx or default_context()
+        if h.dtype != cls.DTYPE:
+            h = h.astype(cls.DTYPE)
+        v = h.view()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_create(ctx.ptr, C.byref(v), C.byref(out)), ctx.ptr)
+        m = cls(out, ctx)
+        m._host = h
+        return m
+
+    @classmethod
+    def new(cls, n: int):
+        return cls.from_host(HostCsr(n, np.zeros(n + 1, np.uint64), [], [], cls.DTYPE))
+
+    @classmethod
+    def identity(cls, n: int):
+        r = np.arange(n, dtype=np.uint64)
+        return cls.from_host(HostCsr(n, np.arange(n + 1, dtype=np.uint64), r, np.ones(n), cls.DTYPE))
+
+    @classmethod
+    def from_coo(cls, n: int, triplets: Iterable):
+        t = np.asarray(list(triplets), dtype=np.float64 if cls.DTYPE == L.F64 else np.uint64).reshape(-1, 3)
+        return cls.from_host(host_from_coo(n, t[:, 0], t[:, 1], t[:, 2], cls.DTYPE))
+
+    @classmethod
+    def from_edges(cls, n: int, edges):
+        e = np.asarray(list(edges), dtype=np.int64).reshape(-1, 2)
+        return cls.from_host(host_from_coo(n, e[:, 0], e[:, 1], np.ones(len(e)), cls.DTYPE))
+
+    @classmethod
+    def from_edges_undirected(cls, n: int, edges):
+        e = np.asarray(list(edges), dtype=np.int64).reshape(-1, 2)
+        off = e[:, 0] != e[:, 1]
+        r = np.concatenate([e[:, 0], e[off, 1]])
+        c = np.concatenate([e[:, 1], e[off, 0]])
+        return cls.from_host(host_from_coo(n, r, c, np.ones(len(r)), cls.DTYPE))
+
+    @classmethod
+    def from_adjacency(cls, it):
+        names, edges = {}, []
+        for a, b in it:
+            ai = names.setdefault(a, len(names))
+            bi = names.setdefault(b, len(names))
+            edges.append((ai, bi))
+        return cls.from_edges(len(names), edges), names
+
+    @classmethod
+    def lattice(cls, dims: Sequence[int], torus: bool):
+        return cls.from_host(host_lattice(dims, torus))
+
+    def thin(self, rng: StdRng, density: float):
+        return type(self).from_host(host_thin(self.host(), rng, density), self._ctx)
+
+    # -- accessors ---------------------------------------------------------------------------------
+    @property
+    def n(self) -> int:
+        return int(self._m.n_rows)
+
+    def nnz(self) -> int:
+        return int(self._m.nnz)
+
+    @property
+    def capacity(self) -> int:
+        return int(self._m.capacity)
+
+    @property
+    def max_row_nnz(self) -> int:
+        return int(self._m.max_row_nnz)
+
+    def view(self) -> L.CsrView:
+        return L.lib().slat_csr_view_of(C.byref(self._m))
+
+    def host(self) -> HostCsr:
+        if self._host is None:
+            n, z, dt = self.n, self.nnz(), int(self._m.dtype)
+            rp = np.empty(n + 1, np.uint64)
+            col = np.empty(max(z, 1), np.uint32)
+            val = np.empty(max(z, 1), _VDT[dt])
+            v = self.view()
+            L.check(L.lib().slat_csr_to_host(self._ctx.ptr, C.byref(v), rp.ctypes.data, col.ctypes.data,
+                                             val.ctypes.data), self._ctx.ptr)
+            self._host = HostCsr(n, rp, col[:z], val[:z], dt)
+        return self._host
+
+    @property
+    def row_ptr(self):
+        return self.host().row_ptr
+
+    @property
+    def col_idx(self):
+        return self.host().col_idx
+
+    @property
+    def values(self):
+        return self.host().values
+
+    def get(self, r: int, c: int):
+        h = self.host()
+        s, e = int(h.row_ptr[r]), int(h.row_ptr[r + 1])
+        i = int(np.searchsorted(h.col_idx[s:e], c))
+        if i < e - s and h.col_idx[s + i] == c:
+            return h.values[s + i].item()
+        return 0
+
+    def row_iter(self, r: int):
+        h = self.host()
+        s, e = int(h.row_ptr[r]), int(h.row_ptr[r + 1])
+        return zip(h.col_idx[s:e].tolist(), h.values[s:e].tolist())
+
+    # -- the hot path --------------------------------------------------------------------------------
+    def _spgemm(self, other: "DeviceCsr", flags: int = 0):
+        if type(other) is not type(self):
+            raise TypeError("operands must have the same matrix type")
+        a, b = self.view(), other.view()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_spgemm(self._ctx.ptr, C.byref(a), C.byref(b), C.byref(out), flags), self._ctx.ptr)
+        return type(self)(out, self._ctx)
+
+    def matmul_rowblock(self, row_begin: int, row_end: int, other: "DeviceCsr", flags: int = 0):
+        a, b = self.view(), other.view()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_spgemm_rowblock(self._ctx.ptr, C.byref(a), row_begin, row_end, C.byref(b),
+                                             C.byref(out), flags), self._ctx.ptr)
+        return type(self)(out, self._ctx)
+
+
+class CsrMatrix(DeviceCsr):
+    """`CsrMatrix` (src/graph_csr.rs:42): u32 node ids, saturating u32 values."""
+
+    DTYPE = L.U32
+
+    def matmul(self, other: "CsrMatrix") -> "CsrMatrix":
+        """CsrMatrix::matmul (src/graph_csr.rs:306-346) on the MI355X engine."""
+        return self._spgemm(other)
+
+    def matmul_par(self, other: "CsrMatrix") -> "CsrMatrix":
+        """CsrMatrix::matmul_par (src/graph_csr.rs:350-484): same result as matmul."""
+        return self._spgemm(other)
+
+
+class MagnusMatrix(DeviceCsr):
+    """`MagnusMatrix` (src/graph_magnus.rs:11): Sat64 values."""
+
+    DTYPE = L.SAT64
+
+    def matmul(self, other: "MagnusMatrix") -> "MagnusMatrix":
+        """MagnusMatrix::matmul (src/graph_magnus.rs:225-232, magnus_spgemm_parallel)."""
+        return self._spgemm(other)
+
+    def matmul_seq(self, other: "MagnusMatrix") -> "MagnusMatrix":
+        """MagnusMatrix::matmul_seq (src/graph_magnus.rs:235-242, magnus_spgemm)."""
+        return self._spgemm(other)
+
+
+class Csr(DeviceCsr):
+    """`linalg::csr::Csr<u32, V>` (linalg/src/csr.rs:93) with V chosen by `dtype`."""
+
+    def __init__(self, owned: L.CsrOwned, ctx: Context):
+        super().__init__(owned, ctx)
+
+    @classmethod
+    def of(cls, dtype: int):
+        return {L.U32: CsrU32, L.SAT64: CsrU64, L.F64: CsrF64}[dtype]
+
+    def matmul(self, other):
+        """Csr::matmul (linalg/src/csr.rs:308-356)."""
+        return self._spgemm(other)
+
+    def matmul_par(self, other):
+        """Csr::matmul_par (linalg/src/csr.rs:361-466)."""
+        return self._spgemm(other)
+
+
+class CsrU32(Csr):
+    DTYPE = L.U32
+
+
+class CsrU64(Csr):
+    DTYPE = L.SAT64
+
+
+class CsrF64(Csr):
+    DTYPE = L.F64

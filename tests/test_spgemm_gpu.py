@@ -1,0 +1,241 @@
+"""Parity of the HIP SpGEMM (through the C ABI) with the oracle and the golden vectors. Needs an
+MI355X: every test is marked `gpu`. Bar: bit-exact arrays for u32 / Sat64 / f64 (the f64 kernel
+reproduces the reference's left fold in A-row order; the tolerance is therefore 0 ulp)."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+import slat
+from helpers import assert_digest, digest
+
+pytestmark = pytest.mark.gpu
+
+DT = {slat.U32: O.U32, slat.SAT64: O.SAT64, slat.F64: O.F64}
+CLS = {slat.U32: slat.CsrMatrix, slat.SAT64: slat.MagnusMatrix, slat.F64: slat.CsrF64}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return slat.default_context(0)
+
+
+def to_dev(o: O.Csr, dtype: int):
+    rp, col, val = o.arrays()
+    return CLS[dtype].from_host(slat.HostCsr(o.n, rp, col, val, dtype))
+
+
+def assert_same(dev, orc: O.Csr, what=""):
+    h = dev.host()
+    rp, col, val = orc.arrays()
+    assert dev.nnz() == orc.nnz, f"{what}: nnz {dev.nnz()} != {orc.nnz}"
+    np.testing.assert_array_equal(h.row_ptr, rp, err_msg=f"{what} row_ptr")
+    np.testing.assert_array_equal(h.col_idx, col, err_msg=f"{what} col_idx")
+    if val.dtype == np.float64:
+        np.testing.assert_array_equal(h.values.view(np.uint64), val.view(np.uint64), err_msg=f"{what} f64 bits")
+    else:
+        np.testing.assert_array_equal(h.values, val, err_msg=f"{what} values")
+
+
+# ---- the reference's own unit tests (src/graph_csr.rs:878-1145, src/graph_magnus.rs:455-697) ----
+@pytest.mark.parametrize("dtype", [slat.U32, slat.SAT64, slat.F64])
+def test_reference_unit_cases(ctx, dtype):
+    M = CLS[dtype]
+    m = M.from_edges(3, [(0, 1), (1, 2)])
+    r = m._spgemm(M.identity(3))
+    assert r.get(0, 1) == 1 and r.get(1, 2) == 1 and r.get(0, 2) == 0 and r.nnz() == 2
+    t = M.from_edges(3, [(0, 1), (1, 2), (2, 0)])
+    t2 = t._spgemm(t)
+    assert t2.get(0, 2) == 1 and t2.get(1, 0) == 1 and t2.get(2, 1) == 1
+    t3 = t2._spgemm(t)
+    assert t3.get(0, 0) == 1 and t3.get(1, 1) == 1 and t3.get(2, 2) == 1
+    assert M.from_edges(2, [(0, 1), (0, 1)]).get(0, 1) == 2
+    d = M.from_edges(4, [(0, 1), (0, 2), (1, 3), (2, 3)])
+    assert d._spgemm(d).get(0, 3) == 2
+    assert M.new(5)._spgemm(M.new(5)).nnz() == 0
+
+
+def test_csr_and_magnus_api_names(ctx):
+    m = slat.CsrMatrix.from_edges(4, [(0, 1), (0, 2), (1, 3), (2, 3)])
+    assert m.matmul(m).get(0, 3) == 2 and m.matmul_par(m).get(0, 3) == 2
+    g = slat.MagnusMatrix.from_edges(4, [(0, 1), (0, 2), (1, 3), (2, 3)])
+    seq, par = g.matmul_seq(g), g.matmul(g)  # test_matmul_seq_vs_par (src/graph_magnus.rs:690-697)
+    assert seq.nnz() == par.nnz() and seq.get(0, 3) == par.get(0, 3) == 2
+
+
+def test_dimension_mismatch_is_an_error(ctx):
+    a, b = slat.CsrMatrix.new(3), slat.CsrMatrix.new(4)
+    with pytest.raises(slat.SlatError) as e:
+        a.matmul(b)
+    assert e.value.status == 2  # SLAT_EDIM where the reference panics
+
+
+# ---- C1/C2: 30^3 torus repeated exponentiation, golden digests ----
+def test_torus30_powers_u32_golden(ctx, golden):
+    A = slat.CsrMatrix.from_host(slat.torus_thinned(30, 3.0, slat.StdRng()))
+    P = A
+    for k in range(2, 8):
+        P = P.matmul(A)
+        h = P.host()
+        assert_digest(digest(h.row_ptr, h.col_idx, h.values), golden["torus30_powers"][k - 1], f"A^{k}")
+
+
+def test_torus30_powers_sat64_and_exact_alloc(ctx, golden):
+    A = slat.MagnusMatrix.from_host(slat.torus_thinned(30, 3.0, slat.StdRng()))
+    P = A
+    for k in range(2, 6):
+        P = P._spgemm(A, slat.FLAG_EXACT_ALLOC if k % 2 else 0)
+        h = P.host()
+        g = golden["torus30_powers"][k - 1]
+        assert_digest(digest(h.row_ptr, h.col_idx, h.values.astype(np.uint32)), g, f"Sat64 A^{k}")
+        assert P.capacity >= P.nnz()
+
+
+# ---- C3: sweep grid, all 20 cells, golden digests of A^2 ----
+def test_sweep_grid_golden(ctx, golden):
+    rng = slat.StdRng()
+    cells = iter(golden["sweep"])
+    for s in [5, 10, 20, 30]:
+        full = slat.host_lattice([s, s, s], True)
+        for epn in [2.0, 3.0, 4.0, 8.0, 26.0]:
+            cell = next(cells)
+            density = epn / (full.nnz / full.n)
+            A = slat.host_thin(full, rng, density) if density < 1.0 else full
+            d = slat.CsrMatrix.from_host(A)
+            C2 = d.matmul(d)
+            h = C2.host()
+            assert_digest(digest(h.row_ptr, h.col_idx, h.values), cell["A2"], f"s={s} epn={epn}")
+
+
+# ---- saturation (test_power_until_stable_chain, src/graph_csr.rs:931-939) ----
+@pytest.mark.parametrize("dtype", [slat.U32, slat.SAT64])
+def test_saturation_chain_matches_oracle(ctx, dtype):
+    n = 64
+    o = O.add(O.from_edges(n, [(i, i + 1) for i in range(n - 1)], DT[dtype]), O.identity(n, DT[dtype]))
+    d = to_dev(o, dtype)
+    for it in range(1, 9):
+        o2 = O.matmul_seq(o, o)
+        d2 = d._spgemm(d)
+        assert_same(d2, o2, f"iteration {it}")
+        o, d = o2, d2
+
+
+def test_large_values_saturate_u32_products(ctx):
+    # products and sums beyond u32::MAX clamp exactly like Saturating<u32>
+    n = 8
+    rows = np.repeat(np.arange(n), n)
+    cols = np.tile(np.arange(n), n)
+    vals = np.full(n * n, 0x10000, dtype=np.uint64)
+    vals[::3] = 0xFFFFFFFF
+    o = O.from_coo(n, rows, cols, vals, O.U32)
+    assert_same(to_dev(o, slat.U32)._spgemm(to_dev(o, slat.U32)), O.matmul_seq(o, o), "u32 sat")
+    vals64 = np.full(n * n, 1 << 40, dtype=np.uint64)
+    vals64[::5] = (1 << 63) + 12345
+    o = O.from_coo(n, rows, cols, vals64, O.SAT64)
+    assert_same(to_dev(o, slat.SAT64)._spgemm(to_dev(o, slat.SAT64)), O.matmul_seq(o, o), "sat64")
+
+
+# ---- f64 (config C5 shape, small): bit-exact left fold ----
+def test_f64_rmat_bit_exact(ctx):
+    h = slat.host_rmat(12, 40000)
+    rp, col, val = h.row_ptr, h.col_idx, h.values
+    o = O.from_arrays(rp, col, val, O.F64)
+    d = slat.CsrF64.from_host(h)
+    assert_same(d.matmul(d), O.matmul_seq(o, o), "rmat f64 A^2")
+    d2 = d.matmul(d)
+    o2 = O.matmul_seq(o, o)
+    assert_same(d2.matmul(d), O.matmul_seq(o2, o), "rmat f64 A^3")
+
+
+def test_f64_cancellation_drops_zeros(ctx):
+    # row 0 of A*B cancels exactly at column 1: the entry must be dropped (linalg/src/csr.rs:344)
+    A = O.from_coo(3, [0, 0, 1], [1, 2, 2], np.array([1.0, 1.0, 2.0]), O.F64)
+    B = O.from_coo(3, [1, 1, 2, 2], [0, 1, 1, 2], np.array([3.0, 1.5, -1.5, 4.0]), O.F64)
+    want = O.matmul_seq(A, B)
+    got = to_dev(A, slat.F64)._spgemm(to_dev(B, slat.F64))
+    assert_same(got, want, "cancellation")
+    assert ctx.stats()["dropped_rows"] == 1
+
+
+def test_explicit_zero_inputs_u32(ctx):
+    # zero values can only enter through raw arrays; the output keeps matmul's zero-free rows
+    rp = np.array([0, 2, 3, 4], np.uint64)
+    col = np.array([0, 1, 2, 1], np.uint32)
+    val = np.array([0, 5, 0, 3], np.uint32)
+    A = slat.CsrMatrix.from_host(slat.HostCsr(3, rp, col, val, slat.U32))
+    h = A.matmul(A).host()
+    dense = np.zeros((3, 3), np.uint64)
+    for r in range(3):
+        for i in range(rp[r], rp[r + 1]):
+            k = col[i]
+            for j in range(rp[k], rp[k + 1]):
+                dense[r, col[j]] += np.uint64(val[i]) * np.uint64(val[j])
+    want_rp = np.concatenate([[0], np.cumsum((dense != 0).sum(1))]).astype(np.uint64)
+    np.testing.assert_array_equal(h.row_ptr, want_rp)
+    np.testing.assert_array_equal(h.col_idx, np.nonzero(dense)[1].astype(np.uint32))
+    np.testing.assert_array_equal(h.values, dense[dense != 0].astype(np.uint32))
+
+
+# ---- kernel paths: wave-per-A-entry (long B rows), rank chunks (>1024 per row), wide windows ----
+def test_wave_mode_long_b_rows(ctx):
+    full = O.lattice([10, 10, 10], True)
+    B = O.matmul_seq(full, full)                     # 125 nnz per row: wave-per-A traversal
+    for dt in (slat.U32, slat.SAT64, slat.F64):
+        a, b = O.convert(full, DT[dt]), O.convert(B, DT[dt])
+        assert_same(to_dev(a, dt)._spgemm(to_dev(b, dt)), O.matmul_seq(a, b), f"wave mode dt={dt}")
+
+
+def test_rank_chunks_long_output_rows(ctx):
+    # a row with 3000 distinct output columns exceeds one LDS value chunk
+    rng = np.random.default_rng(5)
+    n = 4000
+    r = np.concatenate([np.zeros(300, np.int64), rng.integers(0, n, 3000)])
+    c = np.concatenate([rng.choice(n, 300, replace=False), rng.integers(0, n, 3000)])
+    o = O.from_coo(n, r, c, np.ones(len(r)), O.U32)
+    B = O.from_coo(n, rng.integers(0, n, 60000), rng.integers(0, n, 60000), rng.integers(1, 9, 60000), O.U32)
+    for dt in (slat.U32, slat.SAT64, slat.F64):
+        a, b = O.convert(o, DT[dt]), O.convert(B, DT[dt])
+        assert_same(to_dev(a, dt)._spgemm(to_dev(b, dt)), O.matmul_seq(a, b), f"chunks dt={dt}")
+
+
+def test_wide_windows_torus46(ctx):
+    # n = 97,336 columns > one 63,488-column window: rows iterate windows from their min column
+    rng = O.Rng()
+    a = O.torus_thinned(46, 3.0, rng)
+    a2 = O.matmul_seq(a, a)
+    d = to_dev(a, slat.U32)
+    assert_same(d._spgemm(d), a2, "46^3 A^2")
+    assert_same(to_dev(a2, slat.U32)._spgemm(d), O.matmul_seq(a2, a), "46^3 A^3")
+
+
+def test_rowblock_partition_concatenates_to_full(ctx):
+    A = slat.CsrMatrix.from_host(slat.torus_thinned(20, 4.0, slat.StdRng()))
+    full = A.matmul(A).host()
+    n = A.n
+    bounds = [0, n // 3, n // 2, n]
+    cols, vals, rps = [], [], [np.zeros(1, np.uint64)]
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        blk = A.matmul_rowblock(lo, hi, A).host()
+        assert blk.n == hi - lo
+        rps.append(blk.row_ptr[1:] + rps[-1][-1])
+        cols.append(blk.col_idx)
+        vals.append(blk.values)
+    np.testing.assert_array_equal(np.concatenate(rps), full.row_ptr)
+    np.testing.assert_array_equal(np.concatenate(cols), full.col_idx)
+    np.testing.assert_array_equal(np.concatenate(vals), full.values)
+
+
+def test_empty_and_ragged(ctx):
+    for n in (1, 2, 65, 1000):
+        z = slat.CsrMatrix.new(n)
+        assert z.matmul(z).nnz() == 0
+    o = O.from_coo(300, [0, 299, 150], [299, 0, 150], [1, 1, 1], O.U32)
+    d = to_dev(o, slat.U32)
+    assert_same(d._spgemm(d), O.matmul_seq(o, o), "ragged")
+
+
+def test_timing_stats(ctx):
+    A = slat.CsrMatrix.from_host(slat.torus_thinned(30, 3.0, slat.StdRng()))
+    A._spgemm(A, slat.FLAG_TIMING | slat.FLAG_STATS)
+    st = ctx.stats()
+    assert st["nnz"] == 251590 and st["flops"] == 317168
+    assert st["numeric_ms"] > 0 and st["symbolic_ms"] > 0
