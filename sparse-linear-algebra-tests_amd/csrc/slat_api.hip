@@ -270,50 +270,56 @@ extern "C" slat_status slat_csr_max_row_nnz(slat_ctx *ctx, const slat_csr_view *
 // launch helpers (templated over semiring and traversal modes)
 // ---------------------------------------------------------------------------------------------
 template <typename Sem>
-static hipError_t launch_numeric(uint32_t build_mode, uint32_t acc_mode, dim3 grid, size_t lds, hipStream_t s,
-                                 const Args &a) {
-    if constexpr (Sem::kOrdered) {
-        if (build_mode == MODE_LANE_PER_A)
-            hipLaunchKernelGGL((k_numeric<Sem, MODE_LANE_PER_A, MODE_WAVE_PER_A>), grid, dim3(kBlock), lds, s, a);
-        else
-            hipLaunchKernelGGL((k_numeric<Sem, MODE_WAVE_PER_A, MODE_WAVE_PER_A>), grid, dim3(kBlock), lds, s, a);
-    } else {
-        (void)acc_mode;
-        if (build_mode == MODE_LANE_PER_A)
-            hipLaunchKernelGGL((k_numeric<Sem, MODE_LANE_PER_A, MODE_LANE_PER_A>), grid, dim3(kBlock), lds, s, a);
-        else
-            hipLaunchKernelGGL((k_numeric<Sem, MODE_WAVE_PER_A, MODE_WAVE_PER_A>), grid, dim3(kBlock), lds, s, a);
-    }
+static hipError_t launch_numeric(bool idx32, bool sell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
+    if (idx32 && sell)
+        hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true>), grid, dim3(kBlock), lds, s, a);
+    else if (idx32)
+        hipLaunchKernelGGL((k_numeric<Sem, uint32_t, false>), grid, dim3(kBlock), lds, s, a);
+    else if (sell)
+        hipLaunchKernelGGL((k_numeric<Sem, uint64_t, true>), grid, dim3(kBlock), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_numeric<Sem, uint64_t, false>), grid, dim3(kBlock), lds, s, a);
     return hipGetLastError();
 }
 
 template <typename S>
+static hipError_t launch_build_sell(hipStream_t s, const slat_csr_view *B, uint32_t w, uint32_t *scol, void *sval) {
+    const uint64_t blocks = std::min<uint64_t>((B->n_rows + kBlock - 1) / kBlock, 4096);
+    hipLaunchKernelGGL(k_build_sell<S>, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(kBlock), 0, s, B->row_ptr,
+                       B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, w, scol, (S *)sval);
+    return hipGetLastError();
+}
+
+template <typename Sem>
 static hipError_t launch_compact(dim3 grid, hipStream_t s, const uint64_t *orp, const uint64_t *nrp, uint64_t n,
                                  const uint32_t *oc, const void *ov, uint32_t *nc, void *nv) {
-    hipLaunchKernelGGL(k_compact<S>, grid, dim3(kBlock), 0, s, orp, nrp, n, oc, (const S *)ov, nc, (S *)nv);
+    using S = typename Sem::S;
+    hipLaunchKernelGGL(k_compact<Sem>, grid, dim3(kBlock), 0, s, orp, nrp, n, oc, (const S *)ov, nc, (S *)nv);
     return hipGetLastError();
 }
 
 static size_t scan_temp_bytes(uint64_t n) {
     size_t tb = 0;
-    hipcub::DeviceScan::InclusiveSum(nullptr, tb, (const uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, tb, (const uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
     return (tb + 255) & ~(size_t)255;
 }
 
-// Window geometry: ww = 64 * per with `per` odd (lane-contiguous word ownership is then free of
-// LDS bank conflicts). One window covers all columns when n_cols <= 64·31·32.
-static void pick_window(uint64_t ncols, uint32_t &ww, uint32_t &wide) {
+// Window geometry for a group of `threads` lanes: ww = threads * per with `per` odd (thread-
+// contiguous word ownership is then free of LDS bank conflicts) and ww <= max_ww (u16 ranks need
+// 32 * ww <= 65536). `wide` = one window does not cover all columns.
+static void pick_window(uint64_t ncols, uint32_t threads, uint32_t max_ww, uint32_t &ww, uint32_t &wide) {
     const uint64_t words = (ncols + 31) / 32;
-    uint64_t per = (words + kWave - 1) / kWave;
+    uint64_t per = (words + threads - 1) / threads;
     if (per == 0) per = 1;
-    if (per <= 31) {
-        if ((per & 1) == 0) per += 1;
-        wide = 0;
-    } else {
-        per = 31;
+    if ((per & 1) == 0) per += 1;
+    uint64_t max_per = max_ww / threads;
+    if ((max_per & 1) == 0) max_per -= 1;
+    wide = 0;
+    if (per > max_per) {
+        per = max_per;
         wide = 1;
     }
-    ww = (uint32_t)(per * kWave);
+    ww = (uint32_t)(per * threads);
 }
 
 extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
@@ -381,23 +387,38 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.b_val = B->values;
     a.nrows = n;
     a.ncols = ncols;
-    pick_window(ncols, a.ww, a.wide);
-    a.cap = 1024;
     a.stats = (flags & SLAT_FLAG_STATS) ? 1u : 0u;
 
-    const uint32_t build_mode = maxrow_b <= 32 ? MODE_LANE_PER_A : MODE_WAVE_PER_A;
-    const uint32_t acc_mode = dt == SLAT_F64 ? MODE_WAVE_PER_A : build_mode;
+    // 32-bit offsets whenever every position fits (the common case; halves the index math)
+    const bool idx32 = A->nnz < 0xFFFFFFFFull && B->nnz < 0xFFFFFFFFull;
+    Args asym = a;
+    pick_window(ncols, kWave, 1984, asym.ww, asym.wide);
+    pick_window(ncols, kWave, 1984, a.ww, a.wide);
+    a.cap = 512;
+    // slot-major ELL copy of B when its rows are short (SellBatch); bounded blow-up
+    const uint64_t sell_slots = maxrow_b * B->n_rows;
+    const bool sell = maxrow_b <= 64 && sell_slots < (1ull << 31) && sell_slots <= 4 * B->nnz + (1ull << 20);
 
-    // workspace: counts [n] | shards | scan temp
-    const size_t counts_b = ((n * 8) + 255) & ~(size_t)255;
+    // workspace: counts [n] | shards | scan temp | sell col | sell val
+    auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t counts_b = up256(n * 8);
     const size_t shards_b = 4096;
     const size_t scan_b = scan_temp_bytes(n);
-    if ((st = ensure_ws(ctx, counts_b + shards_b + scan_b + 2 * (((n + 1) * 8 + 255) & ~(size_t)255)))) return st;
+    const size_t scol_b = sell ? up256(sell_slots * 4) : 0, sval_b = sell ? up256(sell_slots * vs) : 0;
+    if ((st = ensure_ws(ctx, counts_b + shards_b + scan_b + scol_b + sval_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     a.counts = (uint64_t *)ws;
     a.shards = (unsigned long long *)(ws + counts_b);
     void *scan_tmp = ws + counts_b + shards_b;
     size_t scan_tb = scan_b;
+    uint32_t *scol = (uint32_t *)(ws + counts_b + shards_b + scan_b);
+    void *sval = ws + counts_b + shards_b + scan_b + scol_b;
+    if (sell) {
+        a.sell_w = (uint32_t)maxrow_b;
+        a.sell_n = (uint32_t)B->n_rows;
+        a.sell_col = scol;
+        a.sell_val = sval;
+    }
     a.c_rp = C->row_ptr;
 
     // capacity by exact bound (no mid-call sync) unless it exceeds the budget
@@ -415,23 +436,43 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
 
     // LDS sizing and grid
-    const size_t sym_lds = (size_t)kWavesPerBlock * a.ww * 4;
-    size_t num_lds = (size_t)kWavesPerBlock * numeric_wave_lds(a.ww, a.cap);
-    while (num_lds > ctx->lds_per_block_max && a.cap > 64) {
-        a.cap /= 2;
-        num_lds = (size_t)kWavesPerBlock * numeric_wave_lds(a.ww, a.cap);
-    }
-    const uint64_t want_blocks = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint32_t vsz = dt == SLAT_U32 ? 4 : 8;
+    const int wpb = kBlock / kWave;
+    const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.cap, vsz).bytes;
+    if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
+    const size_t sym_lds = (size_t)wpb * asym.ww * 4;
     const uint64_t max_blocks = (uint64_t)ctx->cu_count * 8;
-    const dim3 grid((unsigned)std::max<uint64_t>(1, std::min(want_blocks, max_blocks)));
+    const dim3 grid((unsigned)std::max<uint64_t>(1, std::min((n + wpb - 1) / wpb, max_blocks)));
+    const dim3 sym_grid = grid;
     const bool timing = flags & SLAT_FLAG_TIMING;
 
     if (a.stats) SLAT_HIP(ctx, hipMemsetAsync(a.shards, 0, 4096, s));
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
-    if (build_mode == MODE_LANE_PER_A)
-        hipLaunchKernelGGL(k_symbolic<MODE_LANE_PER_A>, grid, dim3(kBlock), sym_lds, s, a);
+    asym.counts = a.counts;
+    asym.shards = a.shards;
+    asym.c_rp = a.c_rp;
+    if (sell) {
+        hipError_t be;
+        if (dt == SLAT_U32)
+            be = launch_build_sell<uint32_t>(s, B, a.sell_w, scol, sval);
+        else if (dt == SLAT_SAT64)
+            be = launch_build_sell<unsigned long long>(s, B, a.sell_w, scol, sval);
+        else
+            be = launch_build_sell<double>(s, B, a.sell_w, scol, sval);
+        SLAT_HIP(ctx, be);
+    }
+    asym.sell_w = a.sell_w;
+    asym.sell_n = a.sell_n;
+    asym.sell_col = a.sell_col;
+    asym.sell_val = a.sell_val;
+    if (idx32 && sell)
+        hipLaunchKernelGGL((k_symbolic<uint32_t, true>), sym_grid, dim3(kBlock), sym_lds, s, asym);
+    else if (idx32)
+        hipLaunchKernelGGL((k_symbolic<uint32_t, false>), sym_grid, dim3(kBlock), sym_lds, s, asym);
+    else if (sell)
+        hipLaunchKernelGGL((k_symbolic<uint64_t, true>), sym_grid, dim3(kBlock), sym_lds, s, asym);
     else
-        hipLaunchKernelGGL(k_symbolic<MODE_WAVE_PER_A>, grid, dim3(kBlock), sym_lds, s, a);
+        hipLaunchKernelGGL((k_symbolic<uint64_t, false>), sym_grid, dim3(kBlock), sym_lds, s, asym);
     SLAT_HIP(ctx, hipGetLastError());
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
     SLAT_HIP(ctx, hipcub::DeviceScan::InclusiveSum(scan_tmp, scan_tb, a.counts, C->row_ptr + 1, (int)n, s));
@@ -453,11 +494,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.c_val = C->values;
     hipError_t e;
     if (dt == SLAT_U32)
-        e = launch_numeric<SemU32>(build_mode, acc_mode, grid, num_lds, s, a);
+        e = launch_numeric<SemU32>(idx32, sell, grid, num_lds, s, a);
     else if (dt == SLAT_SAT64)
-        e = launch_numeric<SemSat64>(build_mode, acc_mode, grid, num_lds, s, a);
+        e = launch_numeric<SemSat64>(idx32, sell, grid, num_lds, s, a);
     else
-        e = launch_numeric<SemF64>(build_mode, acc_mode, grid, num_lds, s, a);
+        e = launch_numeric<SemF64>(idx32, sell, grid, num_lds, s, a);
     SLAT_HIP(ctx, e);
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
     SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
@@ -485,10 +526,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, hipMallocAsync((void **)&ncol, std::max<uint64_t>(total, 1) * 4, s));
         SLAT_HIP(ctx, hipMallocAsync(&nval, std::max<uint64_t>(total, 1) * vs, s));
         if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
-        if (vs == 4)
-            e = launch_compact<uint32_t>(grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
+        if (dt == SLAT_U32)
+            e = launch_compact<SemU32>(sym_grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
+        else if (dt == SLAT_SAT64)
+            e = launch_compact<SemSat64>(sym_grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
         else
-            e = launch_compact<uint64_t>(grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
+            e = launch_compact<SemF64>(sym_grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
         SLAT_HIP(ctx, e);
         if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
         (void)hipFreeAsync(C->row_ptr, s);
@@ -513,7 +556,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     S.nnz = nnz;
     S.flops = flops;
     S.capacity = C->capacity;
-    S.mode = build_mode;
+    S.mode = (idx32 ? 1u : 0u) | (sell ? 2u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 counter CSVs: per kernel, the counters of its LAST dispatch (the timed
+workload step in bench.py runs), plus the gfx950 FETCH_SIZE x2 correction (MI355X_MICROARCH.md
+§HBM: FETCH_SIZE reports half the bytes of a wide coalesced read)."""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+
+def load(paths):
+    last = defaultdict(dict)   # kernel -> counter -> value (last dispatch)
+    disp = defaultdict(dict)   # (kernel, dispatch) -> counters
+    for p in paths:
+        with open(p) as f:
+            for r in csv.DictReader(f):
+                k = r["Kernel_Name"]
+                d = int(r["Dispatch_Id"])
+                disp[(k, d)][r["Counter_Name"]] = float(r["Counter_Value"])
+                disp[(k, d)]["_dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                disp[(k, d)]["_lds"] = int(r["LDS_Block_Size"])
+                disp[(k, d)]["_vgpr"] = int(r["VGPR_Count"])
+    for (k, d), c in sorted(disp.items(), key=lambda x: x[0][1]):
+        last[k].update(c)
+    return last
+
+
+def short(k):
+    return k.split("(")[0].replace("void ", "")[:60]
+
+
+if __name__ == "__main__":
+    paths = []
+    for a in sys.argv[1:]:
+        paths += glob.glob(a)
+    last = load(paths)
+    out = {}
+    for k, c in last.items():
+        if "slat" not in k:
+            continue
+        row = dict(c)
+        if "FETCH_SIZE" in row:
+            row["hbm_read_bytes_corrected"] = row["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in row:
+            row["hbm_write_bytes"] = row["WRITE_SIZE"] * 1024
+        out[short(k)] = row
+    print(json.dumps(out, indent=1, sort_keys=True))
