@@ -137,7 +137,7 @@ def main():
         ctx.sync()
 
     barrier()
-    sym, scan, num, tot = [], [], [], []
+    sym, scan, num, tot, abl = [], [], [], [], []
     t0 = time.perf_counter()
     nnz_c = 0
     for _ in range(args.steps):
@@ -145,6 +145,7 @@ def main():
         st = ctx.stats()
         sym.append(st["symbolic_ms"]), scan.append(st["scan_ms"]), num.append(st["numeric_ms"])
         tot.append(st["total_ms"])
+        abl.append(st["compact_ms"])
     barrier()
     elapsed = time.perf_counter() - t0
     stats = ctx.stats()
@@ -166,7 +167,7 @@ def main():
         nnz_a = P.nnz() if row_hi - row_lo == n else int(P.row_ptr[row_hi] - P.row_ptr[row_lo])
         alg = algorithmic_bytes(nnz_a, A.nnz(), nnz_c, row_hi - row_lo, 4)
         num_ms = float(np.mean(num))
-        achieved = alg / (num_ms * 1e-3) / 1e9
+        achieved = alg / (max(num_ms, 1e-6) * 1e-3) / 1e9
         pmc = load_pmc(f"torus{side}_a{power}")
         traffic = pmc.get("numeric_bytes_per_launch") if pmc else None
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -188,7 +189,8 @@ def main():
             "dtype": "u32", "data": "synthetic (reference generator: ChaCha12 StdRng seed [42;32])",
             "config": {"workload": workload, "nnz_c": nnz_c, "n": n, "rows": [row_lo, row_hi],
                        "partition": "block-diagonal, one torus per rank" if args.scaling == "weak" else "flops-balanced row blocks",
-                       "capacity": stats["capacity"], "mode": stats["mode"], "window_words": stats["window_words"]},
+                       "capacity": stats["capacity"], "mode": stats["mode"], "window_words": stats["window_words"],
+                       **({"ablated_ms": round(float(np.mean(abl)), 4)} if os.environ.get("SLAT_ABLATE") else {})},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -270,23 +271,34 @@ extern "C" slat_status slat_csr_max_row_nnz(slat_ctx *ctx, const slat_csr_view *
 // launch helpers (templated over semiring and traversal modes)
 // ---------------------------------------------------------------------------------------------
 template <typename Sem>
-static hipError_t launch_numeric(bool idx32, bool sell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
-    if (idx32 && sell)
+static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
+    if (idx32 && ell)
         hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true>), grid, dim3(kBlock), lds, s, a);
     else if (idx32)
         hipLaunchKernelGGL((k_numeric<Sem, uint32_t, false>), grid, dim3(kBlock), lds, s, a);
-    else if (sell)
+    else if (ell)
         hipLaunchKernelGGL((k_numeric<Sem, uint64_t, true>), grid, dim3(kBlock), lds, s, a);
     else
         hipLaunchKernelGGL((k_numeric<Sem, uint64_t, false>), grid, dim3(kBlock), lds, s, a);
     return hipGetLastError();
 }
 
+static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
+    if (idx32 && ell)
+        hipLaunchKernelGGL((k_symbolic<uint32_t, true>), grid, dim3(kBlock), lds, s, a);
+    else if (idx32)
+        hipLaunchKernelGGL((k_symbolic<uint32_t, false>), grid, dim3(kBlock), lds, s, a);
+    else if (ell)
+        hipLaunchKernelGGL((k_symbolic<uint64_t, true>), grid, dim3(kBlock), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_symbolic<uint64_t, false>), grid, dim3(kBlock), lds, s, a);
+}
+
 template <typename S>
-static hipError_t launch_build_sell(hipStream_t s, const slat_csr_view *B, uint32_t w, uint32_t *scol, void *sval) {
+static hipError_t launch_build_ell(hipStream_t s, const slat_csr_view *B, uint32_t wq, uint32_t *ecol, void *eval) {
     const uint64_t blocks = std::min<uint64_t>((B->n_rows + kBlock - 1) / kBlock, 4096);
-    hipLaunchKernelGGL(k_build_sell<S>, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(kBlock), 0, s, B->row_ptr,
-                       B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, w, scol, (S *)sval);
+    hipLaunchKernelGGL(k_build_ell<S>, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(kBlock), 0, s, B->row_ptr,
+                       B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval);
     return hipGetLastError();
 }
 
@@ -387,38 +399,40 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.b_val = B->values;
     a.nrows = n;
     a.ncols = ncols;
+    a.b_nrows = B->n_rows;
     a.stats = (flags & SLAT_FLAG_STATS) ? 1u : 0u;
 
     // 32-bit offsets whenever every position fits (the common case; halves the index math)
     const bool idx32 = A->nnz < 0xFFFFFFFFull && B->nnz < 0xFFFFFFFFull;
+    uint32_t ablate = 0;  // experiments only: never reaches the real pipeline's kernels
+    if (const char *e_ = std::getenv("SLAT_ABLATE")) ablate = (uint32_t)std::atoi(e_);
     Args asym = a;
     pick_window(ncols, kWave, 1984, asym.ww, asym.wide);
     pick_window(ncols, kWave, 1984, a.ww, a.wide);
     a.cap = 512;
-    // slot-major ELL copy of B when its rows are short (SellBatch); bounded blow-up
-    const uint64_t sell_slots = maxrow_b * B->n_rows;
-    const bool sell = maxrow_b <= 64 && sell_slots < (1ull << 31) && sell_slots <= 4 * B->nnz + (1ull << 20);
+    // padded ELL copy of B when its rows are short (bounded blow-up)
+    const uint64_t wq = (maxrow_b + 3) / 4;
+    const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
+    const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
+                     B->n_rows * wq * 4 < (1ull << 32) && !std::getenv("SLAT_NO_ELL");
 
-    // workspace: counts [n] | shards | scan temp | sell col | sell val
+    // workspace: counts [n] | ablation counts [n] | shards | scan temp | ELL cols | ELL vals
     auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t counts_b = up256(n * 8);
     const size_t shards_b = 4096;
     const size_t scan_b = scan_temp_bytes(n);
-    const size_t scol_b = sell ? up256(sell_slots * 4) : 0, sval_b = sell ? up256(sell_slots * vs) : 0;
-    if ((st = ensure_ws(ctx, counts_b + shards_b + scan_b + scol_b + sval_b))) return st;
+    const size_t ecol_b = ell ? up256(B->n_rows * wq * 16) : 0, eval_b = ell ? up256(B->n_rows * wq * 4 * vs) : 0;
+    if ((st = ensure_ws(ctx, 2 * counts_b + shards_b + scan_b + ecol_b + eval_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
+    if (ell) {
+        a.ell_wq = (uint32_t)wq;
+        a.ell_col = (const uint32_t *)(ws + 2 * counts_b + shards_b + scan_b);
+        a.ell_val = ws + 2 * counts_b + shards_b + scan_b + ecol_b;
+    }
     a.counts = (uint64_t *)ws;
     a.shards = (unsigned long long *)(ws + counts_b);
     void *scan_tmp = ws + counts_b + shards_b;
     size_t scan_tb = scan_b;
-    uint32_t *scol = (uint32_t *)(ws + counts_b + shards_b + scan_b);
-    void *sval = ws + counts_b + shards_b + scan_b + scol_b;
-    if (sell) {
-        a.sell_w = (uint32_t)maxrow_b;
-        a.sell_n = (uint32_t)B->n_rows;
-        a.sell_col = scol;
-        a.sell_val = sval;
-    }
     a.c_rp = C->row_ptr;
 
     // capacity by exact bound (no mid-call sync) unless it exceeds the budget
@@ -436,43 +450,46 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
 
     // LDS sizing and grid
-    const uint32_t vsz = dt == SLAT_U32 ? 4 : 8;
+    const uint32_t vsz = dt == SLAT_SAT64 ? 16 : 8;  // LDS bytes per output slot
     const int wpb = kBlock / kWave;
+    if (const char *e_ = std::getenv("SLAT_CAP")) a.cap = std::max(64, std::atoi(e_));  // tuning knob
     const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.cap, vsz).bytes;
     if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
     const size_t sym_lds = (size_t)wpb * asym.ww * 4;
-    const uint64_t max_blocks = (uint64_t)ctx->cu_count * 8;
+    const uint64_t max_blocks = (uint64_t)ctx->cu_count * 16;
     const dim3 grid((unsigned)std::max<uint64_t>(1, std::min((n + wpb - 1) / wpb, max_blocks)));
     const dim3 sym_grid = grid;
     const bool timing = flags & SLAT_FLAG_TIMING;
 
     if (a.stats) SLAT_HIP(ctx, hipMemsetAsync(a.shards, 0, 4096, s));
-    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
     asym.counts = a.counts;
     asym.shards = a.shards;
     asym.c_rp = a.c_rp;
-    if (sell) {
+    asym.ell_wq = a.ell_wq;
+    asym.ell_col = a.ell_col;
+    asym.ell_val = a.ell_val;
+    if (ell) {
         hipError_t be;
         if (dt == SLAT_U32)
-            be = launch_build_sell<uint32_t>(s, B, a.sell_w, scol, sval);
+            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val);
         else if (dt == SLAT_SAT64)
-            be = launch_build_sell<unsigned long long>(s, B, a.sell_w, scol, sval);
+            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val);
         else
-            be = launch_build_sell<double>(s, B, a.sell_w, scol, sval);
+            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val);
         SLAT_HIP(ctx, be);
     }
-    asym.sell_w = a.sell_w;
-    asym.sell_n = a.sell_n;
-    asym.sell_col = a.sell_col;
-    asym.sell_val = a.sell_val;
-    if (idx32 && sell)
-        hipLaunchKernelGGL((k_symbolic<uint32_t, true>), sym_grid, dim3(kBlock), sym_lds, s, asym);
-    else if (idx32)
-        hipLaunchKernelGGL((k_symbolic<uint32_t, false>), sym_grid, dim3(kBlock), sym_lds, s, asym);
-    else if (sell)
-        hipLaunchKernelGGL((k_symbolic<uint64_t, true>), sym_grid, dim3(kBlock), sym_lds, s, asym);
-    else
-        hipLaunchKernelGGL((k_symbolic<uint64_t, false>), sym_grid, dim3(kBlock), sym_lds, s, asym);
+    if (ablate & 7u) {
+        // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded
+        Args abl = asym;
+        abl.ablate = ablate;
+        abl.counts = (uint64_t *)(ws + counts_b);
+        abl.c_rp = abl.counts;  // row_ptr[0] store lands in scratch too
+        SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
+        launch_symbolic(idx32, ell, sym_grid, sym_lds, s, abl);
+        SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
+    }
+    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
+    launch_symbolic(idx32, ell, sym_grid, sym_lds, s, asym);
     SLAT_HIP(ctx, hipGetLastError());
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
     SLAT_HIP(ctx, hipcub::DeviceScan::InclusiveSum(scan_tmp, scan_tb, a.counts, C->row_ptr + 1, (int)n, s));
@@ -493,12 +510,28 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.c_col = C->col_idx;
     a.c_val = C->values;
     hipError_t e;
+    if (ablate & ~7u) {
+        // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
+        // the real numeric pass below overwrites everything it wrote
+        Args abl = a;
+        abl.ablate = ablate;
+        abl.counts = (uint64_t *)(ws + counts_b);
+        SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
+        if (dt == SLAT_U32)
+            e = launch_numeric<SemU32>(idx32, ell, grid, num_lds, s, abl);
+        else if (dt == SLAT_SAT64)
+            e = launch_numeric<SemSat64>(idx32, ell, grid, num_lds, s, abl);
+        else
+            e = launch_numeric<SemF64>(idx32, ell, grid, num_lds, s, abl);
+        SLAT_HIP(ctx, e);
+        SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
+    }
     if (dt == SLAT_U32)
-        e = launch_numeric<SemU32>(idx32, sell, grid, num_lds, s, a);
+        e = launch_numeric<SemU32>(idx32, ell, grid, num_lds, s, a);
     else if (dt == SLAT_SAT64)
-        e = launch_numeric<SemSat64>(idx32, sell, grid, num_lds, s, a);
+        e = launch_numeric<SemSat64>(idx32, ell, grid, num_lds, s, a);
     else
-        e = launch_numeric<SemF64>(idx32, sell, grid, num_lds, s, a);
+        e = launch_numeric<SemF64>(idx32, ell, grid, num_lds, s, a);
     SLAT_HIP(ctx, e);
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
     SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
@@ -556,7 +589,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     S.nnz = nnz;
     S.flops = flops;
     S.capacity = C->capacity;
-    S.mode = (idx32 ? 1u : 0u) | (sell ? 2u : 0u);
+    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;
@@ -569,6 +602,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         (void)hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]);
         S.numeric_ms = ms;
         S.compact_ms = compact_ms;
+        if (ablate) {
+            (void)hipEventElapsedTime(&ms, ctx->ev[4], ctx->ev[5]);
+            S.compact_ms = ms;  // experiments only: the ablated pass
+        }
         (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]);
         S.total_ms = ms + compact_ms;
     }
