@@ -295,10 +295,11 @@ static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStre
 }
 
 template <typename S>
-static hipError_t launch_build_ell(hipStream_t s, const slat_csr_view *B, uint32_t wq, uint32_t *ecol, void *eval) {
+static hipError_t launch_build_ell(hipStream_t s, const slat_csr_view *B, uint32_t wq, uint32_t *ecol, void *eval,
+                                   uint8_t *eng) {
     const uint64_t blocks = std::min<uint64_t>((B->n_rows + kBlock - 1) / kBlock, 4096);
     hipLaunchKernelGGL(k_build_ell<S>, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(kBlock), 0, s, B->row_ptr,
-                       B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval);
+                       B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng);
     return hipGetLastError();
 }
 
@@ -409,29 +410,33 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     Args asym = a;
     pick_window(ncols, kWave, 1984, asym.ww, asym.wide);
     pick_window(ncols, kWave, 1984, a.ww, a.wide);
-    a.cap = 512;
+    a.cap = 448;  // 3 blocks of 4 waves per CU fit the 160 KB LDS at the 30^3 window (measured best)
     // padded ELL copy of B when its rows are short (bounded blow-up)
     const uint64_t wq = (maxrow_b + 3) / 4;
     const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows * wq * 4 < (1ull << 32) && !std::getenv("SLAT_NO_ELL");
 
-    // workspace: counts [n] | ablation counts [n] | shards | scan temp | ELL cols | ELL vals
+    // workspace: counts [n] | ablation counts [n] | shards | scan temp | ELL cols | ELL vals | ELL groups
     auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t counts_b = up256(n * 8);
-    const size_t shards_b = 4096;
+    const size_t shards_b = 4096 + (SLAT_PHASES ? 8192 : 0);  // + phase-timing slots (diagnostic builds)
     const size_t scan_b = scan_temp_bytes(n);
     const size_t ecol_b = ell ? up256(B->n_rows * wq * 16) : 0, eval_b = ell ? up256(B->n_rows * wq * 4 * vs) : 0;
-    if ((st = ensure_ws(ctx, 2 * counts_b + shards_b + scan_b + ecol_b + eval_b))) return st;
+    const size_t eng_b = ell ? up256(B->n_rows) : 0;
+    const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_scan = o_sh + shards_b, o_ecol = o_scan + scan_b,
+                 o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b;
+    if ((st = ensure_ws(ctx, o_eng + eng_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (ell) {
         a.ell_wq = (uint32_t)wq;
-        a.ell_col = (const uint32_t *)(ws + 2 * counts_b + shards_b + scan_b);
-        a.ell_val = ws + 2 * counts_b + shards_b + scan_b + ecol_b;
+        a.ell_col = (const uint32_t *)(ws + o_ecol);
+        a.ell_val = ws + o_eval;
+        a.ell_ng = ws + o_eng;
     }
     a.counts = (uint64_t *)ws;
-    a.shards = (unsigned long long *)(ws + counts_b);
-    void *scan_tmp = ws + counts_b + shards_b;
+    a.shards = (unsigned long long *)(ws + o_sh);
+    void *scan_tmp = ws + o_scan;
     size_t scan_tb = scan_b;
     a.c_rp = C->row_ptr;
 
@@ -461,28 +466,29 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const dim3 sym_grid = grid;
     const bool timing = flags & SLAT_FLAG_TIMING;
 
-    if (a.stats) SLAT_HIP(ctx, hipMemsetAsync(a.shards, 0, 4096, s));
+    if (a.stats || SLAT_PHASES) SLAT_HIP(ctx, hipMemsetAsync(a.shards, 0, shards_b, s));
     asym.counts = a.counts;
     asym.shards = a.shards;
     asym.c_rp = a.c_rp;
     asym.ell_wq = a.ell_wq;
     asym.ell_col = a.ell_col;
     asym.ell_val = a.ell_val;
+    asym.ell_ng = a.ell_ng;
     if (ell) {
         hipError_t be;
         if (dt == SLAT_U32)
-            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val);
+            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng);
         else if (dt == SLAT_SAT64)
-            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val);
+            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng);
         else
-            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val);
+            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng);
         SLAT_HIP(ctx, be);
     }
     if (ablate & 7u) {
         // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded
         Args abl = asym;
         abl.ablate = ablate;
-        abl.counts = (uint64_t *)(ws + counts_b);
+        abl.counts = (uint64_t *)(ws + o_abl);
         abl.c_rp = abl.counts;  // row_ptr[0] store lands in scratch too
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
         launch_symbolic(idx32, ell, sym_grid, sym_lds, s, abl);
@@ -515,7 +521,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         // the real numeric pass below overwrites everything it wrote
         Args abl = a;
         abl.ablate = ablate;
-        abl.counts = (uint64_t *)(ws + counts_b);
+        abl.counts = (uint64_t *)(ws + o_abl);
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
         if (dt == SLAT_U32)
             e = launch_numeric<SemU32>(idx32, ell, grid, num_lds, s, abl);
@@ -538,6 +544,17 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                                  hipMemcpyDeviceToHost, s));
     SLAT_HIP(ctx, hipStreamSynchronize(s));
 
+    if (SLAT_PHASES) {
+        // diagnostic build: per-phase cycles of the numeric kernel, summed over waves
+        unsigned long long ph[kPhaseSlots * 64];
+        SLAT_HIP(ctx, hipMemcpy(ph, a.shards + 512, sizeof ph, hipMemcpyDeviceToHost));
+        double tot[kPhaseSlots] = {};
+        for (int sh = 0; sh < 64; ++sh)
+            for (int i = 0; i < kPhaseSlots; ++i) tot[i] += (double)ph[sh * kPhaseSlots + i];
+        std::fprintf(stderr, "phases(rows=%.0f):", tot[kPhaseSlots - 1]);
+        for (int i = 0; i < kPhaseSlots - 1; ++i) std::fprintf(stderr, " %d:%.0f", i, tot[i] / std::max(1.0, tot[kPhaseSlots - 1]));
+        std::fprintf(stderr, "\n");
+    }
     uint64_t nnz = ctx->h_shards[0], maxrow = 0, drops = 0, flops = 0;
     for (int i = 0; i < kShards; ++i) {
         maxrow = std::max<uint64_t>(maxrow, ctx->h_shards[i * kShardStride + 1]);

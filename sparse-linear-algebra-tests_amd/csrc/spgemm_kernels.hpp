@@ -35,6 +35,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 namespace slat {
 
@@ -43,6 +44,24 @@ constexpr int kBlock = 256;
 constexpr int kShards = 64;      // sharded status words (avoid one hot atomic address)
 constexpr uint32_t kSent = 0xFFFFFFFFu;  // ELL padding (column ids are < n_cols <= 2^32 - 1)
 constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2] rows with zeros, [3] flops
+
+#ifndef SLAT_PHASES
+#define SLAT_PHASES 0  // diagnostic builds: per-phase s_memtime cycles of k_numeric
+#endif
+constexpr int kPhaseSlots = 16;  // [0..12] phases, [15] rows
+
+// diagnostic builds: s_memtime phase accumulator (compiled away otherwise)
+struct PhaseClock {
+    uint64_t ph[kPhaseSlots];
+    uint64_t t;
+    __device__ __forceinline__ void mark(int i) {
+        if constexpr (SLAT_PHASES) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            ph[i] += now - t;
+            t = now;
+        }
+    }
+};
 
 struct Args {
     const uint64_t *a_rp;
@@ -61,6 +80,7 @@ struct Args {
     uint32_t ablate; // experiments only (SLAT_ABLATE): 1 = symbolic skips its LDS bitmap
     const uint32_t *ell_col;  // [n_B][ell_wq*4] columns, kSent padded
     const void *ell_val;      // [n_B][ell_wq*4] values
+    const uint8_t *ell_ng;    // [n_B] groups of 4 holding real entries: ceil(len / 4)
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
     uint32_t *c_col;
@@ -124,6 +144,17 @@ struct SemF64 {
     __device__ static __forceinline__ bool is_zero(S v) { return v == 0.0; }
 };
 
+// compile-time loop: f(std::integral_constant<int, i>) for i in [0, N) — indices stay constants, so
+// register arrays indexed by them are never demoted to scratch
+template <typename F, int... Is>
+__device__ __forceinline__ void sfor_impl(F &&f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F &&f) {
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 // ------------------------------------------------------------------------------------------------
 // wave / group helpers
 // ------------------------------------------------------------------------------------------------
@@ -137,30 +168,34 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+// Wave64 reductions and scans on DPP (row shifts + row broadcasts): no LDS round trips, unlike
+// __shfl_* (ds_bpermute + a wait per step).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp(uint32_t v, uint32_t identity) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t id, Op op) {
+    v = op(v, dpp<0x111>(v, id));         // row_shr:1
+    v = op(v, dpp<0x112>(v, id));         // row_shr:2
+    v = op(v, dpp<0x114>(v, id));         // row_shr:4
+    v = op(v, dpp<0x118>(v, id));         // row_shr:8
+    v = op(v, dpp<0x142, 0xa>(v, id));    // row_bcast:15 -> rows 1, 3
+    v = op(v, dpp<0x143, 0xc>(v, id));    // row_bcast:31 -> rows 2, 3
     return v;
+}
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l);
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    return readlane_u32(wave_incl_scan(v, 0u, [](uint32_t a, uint32_t b) { return a + b; }), kWave - 1);
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d));
-    return v;
+    return readlane_u32(wave_incl_scan(v, 0u, [](uint32_t a, uint32_t b) { return max(a, b); }), kWave - 1);
 }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d));
-    return v;
+    return readlane_u32(wave_incl_scan(v, 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return min(a, b); }), kWave - 1);
 }
 __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t x) {
-    const int lane = lane_id();
-    uint32_t v = x;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t t = __shfl_up(v, d);
-        if (lane >= d) v += t;
-    }
-    return v - x;
+    return wave_incl_scan(x, 0u, [](uint32_t a, uint32_t b) { return a + b; }) - x;
 }
 __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
@@ -238,9 +273,10 @@ __device__ __forceinline__ void row_span(const Args &p, I a0, I a1, uint64_t &lo
 // ------------------------------------------------------------------------------------------------
 template <typename S>
 __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const uint32_t *col, const S *val,
-                                                       uint32_t n, uint32_t wq, uint32_t *ecol, S *eval) {
+                                                       uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng) {
     for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kBlock) {
         const uint64_t s0 = rp[k], len = rp[k + 1] - s0;
+        eng[k] = (uint8_t)((len + 3) / 4);
         for (uint32_t u = 0; u < wq * 4; ++u) {
             const uint64_t o = k * wq * 4 + u;
             ecol[o] = u < len ? col[s0 + u] : kSent;
@@ -291,28 +327,45 @@ __device__ __forceinline__ Quad<S> quad1(S v) {
     return q;
 }
 
-// grp(c4, v4, a) for every group of B row k, ELL groups from t0 on (CSR: one entry per group)
-template <bool ELL, bool VALS, typename I, typename S, typename G>
-__device__ __forceinline__ void walk_brow(const Args &p, uint32_t k, S a, uint32_t t0, G &&grp) {
+template <typename Sem>
+__device__ __forceinline__ Quad<typename Sem::S> prods(typename Sem::S a, const Quad<typename Sem::S> &v) {
+    Quad<typename Sem::S> pr;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pr.v[e] = Sem::prod(a, v.v[e]);
+    return pr;
+}
+
+// passes that need no values (symbolic, bitmap, column span) walk with this stand-in semiring
+struct SemNone {
+    using S = uint32_t;
+    __device__ static __forceinline__ S prod(S, S) { return 0; }
+};
+
+// grp(c4, pr4) for every group of B row k, ELL groups from t0 on (CSR: one entry per group);
+// pr4 = the products a * b of the group when VALS
+template <typename Sem, bool ELL, bool VALS, typename I, typename G>
+__device__ __forceinline__ void walk_brow(const Args &p, uint32_t k, typename Sem::S a, uint32_t t0, G &&grp) {
+    using S = typename Sem::S;
     if constexpr (ELL) {
         for (uint32_t t = t0; t < p.ell_wq; ++t) {
             const uint4 c = ell_cols(p, k, t);
-            Quad<S> v{};
-            if constexpr (VALS) v = ell_vals<S>(p, k, t);
-            grp(c, v, a);
+            Quad<S> pr{};
+            if constexpr (VALS) pr = prods<Sem>(a, ell_vals<S>(p, k, t));
+            grp(c, pr);
             if (c.w == kSent) break;
         }
     } else {
         const S *bv_ = (const S *)p.b_val;
         const I bs = (I)p.b_rp[k], be = (I)p.b_rp[k + 1];
         for (I jdx = bs; jdx < be; ++jdx)
-            grp(make_uint4(p.b_col[jdx], kSent, kSent, kSent), quad1<S>(VALS ? bv_[jdx] : S(0)), a);
+            grp(make_uint4(p.b_col[jdx], kSent, kSent, kSent), quad1<S>(VALS ? Sem::prod(a, bv_[jdx]) : S(0)));
     }
 }
 
 // Lane-per-A-entry walk of a row: lane l owns entries base + l and base + 64 + l.
-template <bool ELL, bool VALS, typename I, typename S, typename G>
+template <typename Sem, bool ELL, bool VALS, typename I, typename G>
 __device__ __forceinline__ void walk_row(const Args &p, I a0, I a1, G &&grp) {
+    using S = typename Sem::S;
     const int lane = lane_id();
     const S *av_ = (const S *)p.a_val;
     for (I base = a0; base < a1; base += (I)(2 * kWave)) {
@@ -327,8 +380,8 @@ __device__ __forceinline__ void walk_row(const Args &p, I a0, I a1, G &&grp) {
             k1 = p.a_col[i1];
             if constexpr (VALS) a1v = av_[i1];
         }
-        if (k0 < p.b_nrows) walk_brow<ELL, VALS, I, S>(p, k0, a0v, 0, grp);
-        if (k1 < p.b_nrows) walk_brow<ELL, VALS, I, S>(p, k1, a1v, 0, grp);
+        if (k0 < p.b_nrows) walk_brow<Sem, ELL, VALS, I>(p, k0, a0v, 0, grp);
+        if (k1 < p.b_nrows) walk_brow<Sem, ELL, VALS, I>(p, k1, a1v, 0, grp);
     }
 }
 
@@ -381,7 +434,7 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
             bool first = true;
             for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) {
                 uint32_t nprod = 0, x = 0;
-                walk_row<ELL, false, I, uint32_t>(p, a0, a1, [&](uint4 c, const Quad<uint32_t> &, uint32_t) {
+                walk_row<SemNone, ELL, false, I>(p, a0, a1, [&](uint4 c, const Quad<uint32_t> &) {
                     if (p.stats) nprod += (c.x != kSent) + (c.y != kSent) + (c.z != kSent) + (c.w != kSent);
                     if (p.ablate & 1u)
                         x ^= c.x ^ c.y ^ c.z ^ c.w;
@@ -412,24 +465,238 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
 // numeric: one wavefront per row
 // ------------------------------------------------------------------------------------------------
 struct NumLayout {
-    uint32_t off_wb, off_vals, off_cols, bytes;
+    uint32_t off_vals, off_cols, bytes;
 };
 
-// Per-wave LDS region: L0 ww*4 | wbase ww*2 | vals cap*slot_bytes | cols cap*4
+// Per-wave LDS region: W ww*8 (uint2 per bitmap word: .x column bits, .y rank of the word's first
+// column, so a rank lookup is ONE ds_read_b64) | vals cap*slot_bytes | cols cap*4
 __host__ __device__ inline NumLayout num_layout(uint32_t ww, uint32_t cap, uint32_t slot_bytes) {
     auto up = [](uint32_t x, uint32_t a) { return (x + a - 1) / a * a; };
     NumLayout L;
-    L.off_wb = ww * 4;
-    L.off_vals = up(L.off_wb + ww * 2, 16);
+    L.off_vals = up(ww * 8, 16);
     L.off_cols = up(L.off_vals + cap * slot_bytes, 16);
     L.bytes = up(L.off_cols + cap * 4, 16);
     return L;
 }
 
+// rank (within chunk [r0, r0 + nch)) of column c, or kSent. The LDS read happens for every lane
+// (word 0 for columns outside the window) and the predicate is a non-short-circuit AND on the
+// loaded value, so a batch issues all its lookups before it waits on any.
+__device__ __forceinline__ uint2 rank_word(const uint2 *W, uint32_t c, uint32_t wlo, uint32_t WIN, uint32_t &off,
+                                           bool &ok) {
+    ok = win_off(c, wlo, WIN, off);
+    return W[ok ? (off >> 5) : 0u];
+}
+__device__ __forceinline__ uint32_t rank_in(uint2 w, uint32_t off, bool ok, uint32_t r0, uint32_t nch) {
+    const uint32_t r = w.y + __popc(w.x & ((1u << (off & 31)) - 1u)) - r0;
+    return (ok & (r < nch)) ? r : kSent;
+}
+
 constexpr int kRegQ = 4;  // A entries per lane kept in registers across the numeric passes
 
+template <typename S>
+__device__ __forceinline__ S permute_val(int dst, S v) {
+    if constexpr (sizeof(S) == 4) {
+        return __builtin_bit_cast(S, __builtin_amdgcn_ds_permute(dst, __builtin_bit_cast(int, v)));
+    } else {
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)u);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(u >> 32));
+        return __builtin_bit_cast(S, ((uint64_t)hi << 32) | lo);
+    }
+}
+
+// materialise v in VGPRs here (an empty asm consuming it): stops the compiler from sinking the
+// load that produces v into a later conditional block
+template <typename T>
+__device__ __forceinline__ void pin(T &v) {
+    if constexpr (sizeof(T) == 4) {
+        asm volatile("" : "+v"(v));
+    } else {
+        uint64_t u = __builtin_bit_cast(uint64_t, v);
+        uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+        asm volatile("" : "+v"(lo), "+v"(hi));
+        v = __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
+    }
+}
+
+// Compaction of per-lane work items (k, a) into full 64-lane batches with ds_permute: the lanes
+// that hold an item send it to consecutive lanes of the batch; a full batch is handed to `run`
+// (every lane one item, kSent = none). Masked-off lanes cost an LDS instruction nearly as much as
+// active ones, so ragged tails are processed dense.
+template <typename S>
+struct TailBatch {
+    uint32_t filled = 0, bk = kSent;
+    S ba = S(0);
+    template <typename F>
+    __device__ __forceinline__ void add(bool has, uint32_t k, S a, F &&run) {
+        const int lane = lane_id();
+        unsigned long long m = __ballot(has);
+        while (m) {
+            const uint32_t n = __popcll(m);
+            const uint32_t taken = min(n, (uint32_t)kWave - filled);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint32_t pos = filled + below;
+            const bool go = has && pos < filled + taken;
+            // senders write to consecutive receiving lanes; the rest to a lane outside the
+            // receiving range (there is one whenever any lane is not sending)
+            const int dst = (int)((go ? pos : ((filled + taken) & (kWave - 1))) * 4);
+            const uint32_t rk = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)k);
+            const S ra = permute_val(dst, a);
+            if ((uint32_t)lane >= filled && (uint32_t)lane < filled + taken) {
+                bk = rk;
+                ba = ra;
+            }
+            filled += taken;
+            has = has && !go;
+            m = __ballot(has);
+            if (filled == kWave) {
+                run(bk, ba);
+                filled = 0;
+                bk = kSent;
+            }
+        }
+    }
+    template <typename F>
+    __device__ __forceinline__ void flush(F &&run) {
+        if (filled) run(bk, ba);
+        filled = 0;
+        bk = kSent;
+    }
+};
+
+// Every compacted tail batch (ELL groups t >= 1 of the A entries the lanes hold), in a fixed order:
+// fn(bi, c4, pr4) for the batches bi with want(bi); returns the number of batches.
+template <typename Sem, bool VALS, typename Wt, typename F>
+__device__ __forceinline__ uint32_t for_tails(const Args &p, const uint32_t *kq, const typename Sem::S *aq,
+                                              const uint32_t *ngq, uint32_t mx, Wt &&want, F &&fn) {
+    using S = typename Sem::S;
+    uint32_t bi = 0;
+    for (uint32_t t = 1; t < mx; ++t) {
+        TailBatch<S> tb;
+        auto run = [&](uint32_t k, S a) {
+            if (want(bi)) {
+                uint4 c = make_uint4(kSent, kSent, kSent, kSent);
+                Quad<S> pr{};
+                if (k != kSent) {
+                    c = ell_cols(p, k, t);
+                    if constexpr (VALS) pr = prods<Sem>(a, ell_vals<S>(p, k, t));
+                }
+                fn(bi, c, pr);
+            }
+            ++bi;
+        };
+#pragma unroll
+        for (int q = 0; q < kRegQ; ++q) tb.add(ngq[q] > t, kq[q], aq[q], run);
+        tb.flush(run);
+    }
+    return bi;
+}
+
+// numeric pass 1: column span of the row (rows wider than one window)
+template <typename S>
+struct SpanPass {
+    uint32_t l = 0xFFFFFFFFu, h = 0;
+    __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &) {
+        const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (cc[e] != kSent) {
+                l = min(l, cc[e]);
+                h = max(h, cc[e]);
+            }
+    }
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
+        sfor<kRegQ>([&](auto Q) { (*this)(c[Q], pr[Q]); });
+    }
+};
+
+// numeric pass 2: the window's column bitmap (W[w].x), fire-and-forget LDS atomics
+template <typename S>
+struct BitmapPass {
+    uint32_t *L0;  // L0[2w] aliases W[w].x
+    uint32_t wlo, WIN;
+    __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &) {
+        const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t off;
+            if (win_off(cc[e], wlo, WIN, off)) atomicOr(&L0[(off >> 5) * 2], 1u << (off & 31));
+        }
+    }
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
+        sfor<kRegQ>([&](auto Q) { (*this)(c[Q], pr[Q]); });
+    }
+};
+
+// numeric pass 3: accumulate products into rank slots; all rank lookups of a batch first
+template <typename Sem>
+struct AccPass {
+    using S = typename Sem::S;
+    const uint2 *W;
+    typename Sem::V *vals;
+    uint32_t *cols;
+    uint32_t wlo, WIN, r0, nch;
+    PhaseClock *pc;
+    uint32_t abl;  // experiments: 64 no column stores, 128 no value atomics, 256 hashed ranks (no reads)
+    template <int Q>
+    __device__ __forceinline__ void run(const uint4 *c, const Quad<S> *pr_in) {
+        uint2 w[Q][4];
+        uint32_t off[Q][4];
+        bool ok[Q][4];
+        S pr[Q][4];
+        // products pinned in VGPRs up front: keeps B-value loads out of the per-slot branches
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                pr[q][e] = pr_in[q].v[e];
+                pin(pr[q][e]);
+            }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t cc[4] = {c[q].x, c[q].y, c[q].z, c[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (abl & 256u) {
+                    ok[q][e] = win_off(cc[e], wlo, WIN, off[q][e]);
+                    w[q][e] = make_uint2(0xFFFFFFFFu, (cc[e] * 2654435761u) >> 23);
+                } else {
+                    w[q][e] = rank_word(W, cc[e], wlo, WIN, off[q][e], ok[q][e]);
+                }
+            }
+        }
+        if constexpr (SLAT_PHASES) {
+            pin(w[0][0].x);
+            pc->mark(10);  // rank reads
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t cc[4] = {c[q].x, c[q].y, c[q].z, c[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t r = rank_in(w[q][e], off[q][e], ok[q][e], r0, nch);
+                if (r != kSent) {
+                    if (!(abl & 128u)) Sem::acc(vals, r, pr[q][e]);
+                    if (!(abl & 64u)) cols[r] = cc[e];
+                }
+            }
+        }
+        if constexpr (SLAT_PHASES) pc->mark(11);  // atomics issued
+    }
+    __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) { run<1>(&c, &pr); }
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
+        sfor<kRegQ / 2>([&](auto H) { run<2>(c + 2 * H, pr + 2 * H); });
+    }
+};
+
+#ifndef SLAT_NUM_ATTR
+#define SLAT_NUM_ATTR
+#endif
+constexpr uint32_t kNB = 2;  // compacted tail batches kept in registers per row (ct0/ct1)
+
 template <typename Sem, typename I, bool ELL>
-__global__ __launch_bounds__(kBlock) void k_numeric(Args p) {
+__global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     using S = typename Sem::S;
     using V = typename Sem::V;
     constexpr int kWpb = kBlock / kWave;
@@ -441,15 +708,15 @@ __global__ __launch_bounds__(kBlock) void k_numeric(Args p) {
     const int wv = threadIdx.x / kWave;
     const NumLayout lay = num_layout(p.ww, p.cap, sizeof(V) * Sem::kSlots);
     uint8_t *region = smem8 + (size_t)wv * lay.bytes;
-    uint32_t *L0 = (uint32_t *)region;
-    uint16_t *wbase = (uint16_t *)(region + lay.off_wb);
+    uint2 *W = (uint2 *)region;
+    uint32_t *L0 = (uint32_t *)region;  // L0[2w] aliases W[w].x
     V *vals = (V *)(region + lay.off_vals);
     uint32_t *cols = (uint32_t *)(region + lay.off_cols);
     S *cval = (S *)p.c_val;
     const S *av_ = (const S *)p.a_val;
 
     if (blockIdx.x == 0 && threadIdx.x == 0) p.shards[0] = p.c_rp[p.nrows];
-    for (uint32_t w = lane; w < p.ww; w += kWave) L0[w] = 0;
+    for (uint32_t w = lane; w < p.ww; w += kWave) W[w] = make_uint2(0u, 0u);
     wave_sync();
 
     const uint32_t WIN = p.ww * 32;
@@ -457,75 +724,144 @@ __global__ __launch_bounds__(kBlock) void k_numeric(Args p) {
     const uint32_t wb0 = lane * per;
     uint32_t maxrow = 0, zrows = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
+    PhaseClock pc{};
+    if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
+    auto mark = [&](int i) { pc.mark(i); };
+    uint64_t *ph = pc.ph;
     for (uint64_t row = (uint64_t)blockIdx.x * kWpb + wv; row < p.nrows; row += stride) {
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         const uint64_t out_begin = p.c_rp[row], out_end = p.c_rp[row + 1];
         uint64_t out_pos = out_begin;
         uint32_t zeros = 0;
+        ph[kPhaseSlots - 1] += 1;
         if (a1 > a0) {
-            // rows of up to 64*kRegQ A entries keep their A entries in registers for both passes
-            const bool single = (uint64_t)(a1 - a0) <= (uint64_t)(kWave * kRegQ);
-            uint32_t kq[kRegQ];
+            // A entries are taken in segments of 64*kRegQ held by the lanes (kq/aq). With the ELL
+            // copy of B, a segment's later groups (entry, t >= 1) of ALL rounds are compacted into at
+            // most kNB dense 64-lane batches of (B row, group, a) in registers, so a pass issues all
+            // of a segment's group loads at once (one L2 round trip). One-segment rows keep their
+            // segment across passes; longer rows rebuild it per pass.
+            constexpr uint32_t kSeg = kWave * kRegQ;
+            constexpr uint32_t kOvf = 0xFFFFFFFFu;  // segment with more tail items than kNB batches
+            const uint64_t len = (uint64_t)(a1 - a0);
+            const uint32_t nseg = (uint32_t)((len + kSeg - 1) / kSeg);
+            const bool single = nseg == 1;
+            uint32_t kq[kRegQ], ngq[kRegQ];
             S aq[kRegQ];
-#pragma unroll
-            for (int q = 0; q < kRegQ; ++q) {
-                const I idx = a0 + (I)(q * kWave + lane);
-                kq[q] = kSent;
-                aq[q] = S(0);
-                if (single && idx < a1) {
-                    kq[q] = p.a_col[idx];
-                    if (kq[q] >= p.b_nrows) kq[q] = kSent;  // malformed input: ignore the entry
-                    if constexpr (kVals) aq[q] = av_[idx];
+            uint32_t bk0 = kSent, bk1 = kSent, bt0 = 0, bt1 = 0, nb = 0;
+            S ba0 = S(0), ba1 = S(0);
+            auto load_seg = [&](I sb) {
+                // bare loads inside the branches, all arithmetic on them after: a use inside the
+                // branch would make the wave wait there, serialising the q loads
+                sfor<kRegQ>([&](auto Q) {
+                    constexpr int q = Q;
+                    const I idx = sb + (I)(q * kWave + lane);
+                    kq[q] = kSent;
+                    aq[q] = S(0);
+                    if (idx < a1) {
+                        kq[q] = p.a_col[idx];
+                        if constexpr (kVals) aq[q] = av_[idx];
+                    }
+                });
+                sfor<kRegQ>([&](auto Q) {
+                    if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
+                });
+                if constexpr (!ELL) return;
+                uint32_t mx = 0;
+                sfor<kRegQ>([&](auto Q) {
+                    constexpr int q = Q;
+                    ngq[q] = kq[q] != kSent ? p.ell_ng[kq[q]] : 0u;
+                    mx = max(mx, ngq[q]);
+                });
+                mx = wave_max_u32(mx);
+                bk0 = bk1 = kSent;
+                uint32_t off = 0;  // items placed so far (uniform)
+                for (uint32_t t = 1; t < mx; ++t) {
+                    sfor<kRegQ>([&](auto Q) {
+                        constexpr int q = Q;
+                        const bool has = ngq[q] > t;
+                        const unsigned long long m = __ballot(has);
+                        const uint32_t cnt = __popcll(m);
+                        if (cnt == 0) return;
+                        const uint32_t below =
+                            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        // senders go to lanes (off + rank) mod 64; the rest to a lane outside that
+                        // range (one exists unless all 64 lanes send)
+                        const int dst = (int)(((has ? off + below : off + cnt) & (kWave - 1)) * 4);
+                        const uint32_t rk = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)kq[q]);
+                        const S ra = permute_val(dst, aq[q]);
+                        const uint32_t i = ((uint32_t)lane - off) & (kWave - 1);  // receive slot
+                        const uint32_t g = off + i;  // global item index -> batch g / 64
+                        // value selects, not conditional stores: keeps the batch registers in VGPRs
+                        const bool in0 = (i < cnt) & (g < (uint32_t)kWave);
+                        const bool in1 = (i < cnt) & (g >= (uint32_t)kWave) & (g < 2u * kWave);
+                        bk0 = in0 ? rk : bk0;
+                        ba0 = in0 ? ra : ba0;
+                        bt0 = in0 ? t : bt0;
+                        bk1 = in1 ? rk : bk1;
+                        ba1 = in1 ? ra : ba1;
+                        bt1 = in1 ? t : bt1;
+                        off += cnt;
+                    });
                 }
-            }
-            // every group of the row: the first group of every register-resident A entry is
-            // loaded for all q before any is consumed, then the tails
+                nb = (off + kWave - 1) / kWave;
+                if (nb > kNB) nb = kOvf;
+            };
+            if (single) load_seg(a0);
+            if constexpr (SLAT_PHASES) pin(kq[0]);  // wait for the A entries inside phase 0
+            mark(0);  // row bounds + A entries, group counts, tail compaction
+            // every group of the row, as (columns, products)
             auto each_group = [&](auto &&grp, auto vals_tag) {
                 constexpr bool VV = decltype(vals_tag)::value;
-                if (single) {
-                    if constexpr (ELL) {
-                        uint4 cq[kRegQ];
-                        Quad<S> vq[kRegQ];
-#pragma unroll
-                        for (int q = 0; q < kRegQ; ++q) {
+                if constexpr (ELL) {
+                    for (uint32_t sg = 0; sg < nseg; ++sg) {
+                        if (!single) load_seg(a0 + (I)((uint64_t)sg * kSeg));
+                        if (nb == kOvf) {  // rare: too many tail items for the register batches
+                            sfor<kRegQ>([&](auto Q) {
+                                if (kq[Q] != kSent) walk_brow<Sem, true, VV, I>(p, kq[Q], aq[Q], 0, grp);
+                            });
+                            continue;
+                        }
+                        // every load of the segment issued before any is used (bare loads in the
+                        // branches; products computed after, unconditionally)
+                        uint4 cq[kRegQ], ct0 = make_uint4(kSent, kSent, kSent, kSent), ct1 = ct0;
+                        Quad<S> pq[kRegQ], pt0{}, pt1{};
+                        sfor<kRegQ>([&](auto Q) {
+                            constexpr int q = Q;
                             cq[q] = make_uint4(kSent, kSent, kSent, kSent);
-                            vq[q] = Quad<S>{};
+                            pq[q] = Quad<S>{};
                             if (kq[q] != kSent) {
                                 cq[q] = ell_cols(p, kq[q], 0);
-                                if constexpr (VV) vq[q] = ell_vals<S>(p, kq[q], 0);
+                                if constexpr (VV) pq[q] = ell_vals<S>(p, kq[q], 0);
                             }
+                        });
+                        if (bk0 != kSent) {
+                            ct0 = ell_cols(p, bk0, bt0);
+                            if constexpr (VV) pt0 = ell_vals<S>(p, bk0, bt0);
                         }
-                        grp.multi(cq, vq, aq);
-#pragma unroll
-                        for (int q = 0; q < kRegQ; ++q)
-                            if (cq[q].w != kSent) walk_brow<true, VV, I, S>(p, kq[q], aq[q], 1, grp);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < kRegQ; ++q)
-                            if (kq[q] != kSent) walk_brow<false, VV, I, S>(p, kq[q], aq[q], 0, grp);
+                        if (bk1 != kSent) {
+                            ct1 = ell_cols(p, bk1, bt1);
+                            if constexpr (VV) pt1 = ell_vals<S>(p, bk1, bt1);
+                        }
+                        if constexpr (VV) {
+                            sfor<kRegQ>([&](auto Q) { pq[Q] = prods<Sem>(aq[Q], pq[Q]); });
+                            pt0 = prods<Sem>(ba0, pt0);
+                            pt1 = prods<Sem>(ba1, pt1);
+                        }
+                        grp.multi(cq, pq);
+                        if (nb > 0) grp(ct0, pt0);
+                        if (nb > 1) grp(ct1, pt1);
                     }
+                } else if (single) {
+                    sfor<kRegQ>([&](auto Q) {
+                        if (kq[Q] != kSent) walk_brow<Sem, false, VV, I>(p, kq[Q], aq[Q], 0, grp);
+                    });
                 } else {
-                    walk_row<ELL, VV, I, S>(p, a0, a1, grp);
+                    walk_row<Sem, false, VV, I>(p, a0, a1, grp);
                 }
             };
             uint64_t lo = 0, hi = p.ncols - 1;
             if (p.wide) {
-                struct MinMax {
-                    uint32_t l = 0xFFFFFFFFu, h = 0;
-                    __device__ void operator()(uint4 c, const Quad<S> &, S) {
-                        const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (cc[e] != kSent) {
-                                l = min(l, cc[e]);
-                                h = max(h, cc[e]);
-                            }
-                    }
-                    __device__ void multi(const uint4 *c, const Quad<S> *v, const S *a) {
-#pragma unroll
-                        for (int q = 0; q < kRegQ; ++q) (*this)(c[q], v[q], a[q]);
-                    }
-                } mm;
+                SpanPass<S> mm;
                 each_group(mm, std::false_type{});
                 const uint32_t l = wave_min_u32(mm.l), h = wave_max_u32(mm.h);
                 lo = l;
@@ -537,94 +873,51 @@ __global__ __launch_bounds__(kBlock) void k_numeric(Args p) {
             }
             for (uint64_t wlo64 = lo & ~31ull; wlo64 <= hi; wlo64 += WIN) {
                 const uint32_t wlo = (uint32_t)wlo64;
-                // 1. column bitmap of the window
-                struct Or4 {
-                    uint32_t *L0;
-                    uint32_t wlo, WIN;
-                    __device__ void operator()(uint4 c, const Quad<S> &, S) { bitmap_or4(L0, c, wlo, WIN); }
-                    __device__ void multi(const uint4 *c, const Quad<S> *, const S *) {
-#pragma unroll
-                        for (int q = 0; q < kRegQ; ++q) bitmap_or4(L0, c[q], wlo, WIN);
-                    }
-                } or4{L0, wlo, WIN};
-                if (!(p.ablate & 32u)) each_group(or4, std::false_type{});
+                // 1. column bitmap of the window (into W[w].x)
+                BitmapPass<S> bm{L0, wlo, WIN};
+                if (!(p.ablate & 32u)) each_group(bm, std::false_type{});
                 wave_sync();
-                // 2. word ranks (lane owns words [wb0, wb0 + per))
+                (void)__builtin_amdgcn_readfirstlane(L0[0]);
+                mark(1);  // bitmap pass
+                // 2. word ranks (lane owns words [wb0, wb0 + per)) into W[w].y
                 uint32_t lc = 0;
-                for (uint32_t q = 0; q < per; ++q) lc += __popc(L0[wb0 + q]);
+                for (uint32_t q = 0; q < per; ++q) lc += __popc(W[wb0 + q].x);
                 const uint32_t ex = wave_excl_scan_u32(lc);
                 const uint32_t wcnt = readlane_u32(ex + lc, kWave - 1);
                 if (wcnt == 0) continue;  // bitmap empty: nothing to clear
                 {
                     uint32_t run = ex;
                     for (uint32_t q = 0; q < per; ++q) {
-                        wbase[wb0 + q] = (uint16_t)run;
-                        run += __popc(L0[wb0 + q]);
+                        W[wb0 + q].y = run;
+                        run += __popc(W[wb0 + q].x);
                     }
                 }
-                wave_sync();
+                mark(2);  // word ranks
                 for (uint32_t r0 = 0; r0 < wcnt; r0 += p.cap) {
                     const uint32_t nch = min(p.cap, wcnt - r0);
                     for (uint32_t t = lane; t < nch * Sem::kSlots; t += kWave) vals[t] = V(0);
                     wave_sync();
-                    // rank of column c in this chunk, or kSent; the two LDS reads are unconditional
-                    auto rank_of = [&](uint32_t c) -> uint32_t {
-                        uint32_t off;
-                        const bool ok = win_off(c, wlo, WIN, off);
-                        const uint32_t w = ok ? (off >> 5) : 0u;
-                        const uint32_t r = (uint32_t)wbase[w] + __popc(L0[w] & ((1u << (off & 31)) - 1u)) - r0;
-                        return (ok && r < nch) ? r : kSent;
-                    };
-                    // 3. values + the column of every rank (duplicates store the same column)
+                    mark(8);  // zero value slots
+                    // 3. values and the column of every rank (duplicates store the same column)
                     if constexpr (Sem::kOrdered) {
                         if (!(p.ablate & 8u))
                             traverse_ordered<I, S>(p, a0, a1, [&](uint32_t j, S a, S b) {
-                                const uint32_t r = rank_of(j);
+                                uint32_t off;
+                                bool ok;
+                                const uint2 w = rank_word(W, j, wlo, WIN, off, ok);
+                                const uint32_t r = rank_in(w, off, ok, r0, nch);
                                 if (r != kSent) {
                                     Sem::acc(vals, r, Sem::prod(a, b));
                                     cols[r] = j;
                                 }
                             });
                     } else if (!(p.ablate & 8u)) {
-                        struct Acc4 {
-                            decltype(rank_of) &rk;
-                            V *vals;
-                            uint32_t *cols;
-                            __device__ void operator()(uint4 c, const Quad<S> &v, S a) {
-                                const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
-                                uint32_t r[4];
-#pragma unroll
-                                for (int e = 0; e < 4; ++e) r[e] = rk(cc[e]);
-#pragma unroll
-                                for (int e = 0; e < 4; ++e)
-                                    if (r[e] != kSent) {
-                                        Sem::acc(vals, r[e], Sem::prod(a, v.v[e]));
-                                        cols[r[e]] = cc[e];
-                                    }
-                            }
-                            __device__ void multi(const uint4 *c, const Quad<S> *v, const S *a) {
-                                uint32_t r[kRegQ][4];
-#pragma unroll
-                                for (int q = 0; q < kRegQ; ++q) {
-                                    const uint32_t cc[4] = {c[q].x, c[q].y, c[q].z, c[q].w};
-#pragma unroll
-                                    for (int e = 0; e < 4; ++e) r[q][e] = rk(cc[e]);
-                                }
-#pragma unroll
-                                for (int q = 0; q < kRegQ; ++q) {
-                                    const uint32_t cc[4] = {c[q].x, c[q].y, c[q].z, c[q].w};
-#pragma unroll
-                                    for (int e = 0; e < 4; ++e)
-                                        if (r[q][e] != kSent) {
-                                            Sem::acc(vals, r[q][e], Sem::prod(a[q], v[q].v[e]));
-                                            cols[r[q][e]] = cc[e];
-                                        }
-                                }
-                            }
-                        } acc4{rank_of, vals, cols};
-                        each_group(acc4, std::integral_constant<bool, kVals>{});
+                        AccPass<Sem> acc{W, vals, cols, wlo, WIN, r0, nch, &pc, p.ablate};
+                        each_group(acc, std::true_type{});
                     }
                     wave_sync();
+                    if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
+                    mark(12);  // accumulate pass drain
                     // 4. emit at the row's slice, coalesced
                     for (uint32_t t = lane; t < nch; t += kWave) {
                         const S v = Sem::finish(vals, t);
@@ -636,16 +929,25 @@ __global__ __launch_bounds__(kBlock) void k_numeric(Args p) {
                     }
                     out_pos += nch;
                     wave_sync();
+                    mark(4);  // emit
                 }
-                for (uint32_t q = 0; q < per; ++q) L0[wb0 + q] = 0;
+                for (uint32_t q = 0; q < per; ++q) W[wb0 + q].x = 0;
                 wave_sync();
             }
         }
+        mark(5);  // window clears, empty rows
         const uint32_t rz = p.ablate ? 0u : wave_sum_u32(zeros);  // ablation runs: no compaction
         const uint64_t got = out_pos - out_begin - rz;
         if (lane == 0) p.counts[row] = got;
         maxrow = max(maxrow, (uint32_t)min<uint64_t>(got, 0xFFFFFFFFull));
         zrows += rz ? 1u : 0u;
+    }
+    mark(6);  // row tail (counts)
+    if constexpr (SLAT_PHASES) {
+        if (lane == 0) {
+            unsigned long long *dst = p.shards + 512 + ((blockIdx.x * kWpb + wv) % 64) * kPhaseSlots;
+            for (int i = 0; i < kPhaseSlots; ++i) atomicAdd(&dst[i], (unsigned long long)ph[i]);
+        }
     }
     if (lane == 0) {
         red[0][wv] = maxrow;

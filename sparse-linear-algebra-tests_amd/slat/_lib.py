@@ -7,7 +7,8 @@ import os
 import subprocess
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libslat.so")
+# SLAT_LIB_PATH: load another build of the same library (kernel experiments); default in-tree
+LIB_PATH = os.environ.get("SLAT_LIB_PATH") or os.path.join(PKG_DIR, "libslat.so")
 
 SLAT_OK, SLAT_EINVAL, SLAT_EDIM, SLAT_EOOM, SLAT_EHIP, SLAT_ENOTSUP, SLAT_ENODEV = range(7)
 U32, SAT64, F64 = 0, 1, 2

@@ -33,7 +33,7 @@ def short(k):
 if __name__ == "__main__":
     paths = []
     for a in sys.argv[1:]:
-        paths += glob.glob(a)
+        paths += glob.glob(a, recursive=True)
     last = load(paths)
     out = {}
     for k, c in last.items():
