@@ -34,6 +34,8 @@ struct slat_ctx {
     void *ws = nullptr;
     size_t ws_bytes = 0;
     unsigned long long *h_shards = nullptr;  // pinned
+    unsigned long long *d_vmax = nullptr;    // (epoch << 32) | max B value, written by k_build_ell
+    uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
     hipEvent_t ev[6] = {};
     slat_stats stats = {};
 };
@@ -99,6 +101,12 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         delete ctx;
         return SLAT_EOOM;
     }
+    if (hipMalloc((void **)&ctx->d_vmax, 8) != hipSuccess || hipMemset(ctx->d_vmax, 0, 8) != hipSuccess) {
+        (void)hipHostFree(ctx->h_shards);
+        (void)hipStreamDestroy(ctx->own_stream);
+        delete ctx;
+        return SLAT_EOOM;
+    }
     for (auto &e : ctx->ev) (void)hipEventCreate(&e);
     *out = ctx;
     return SLAT_OK;
@@ -110,6 +118,7 @@ slat_status slat_ctx_destroy(slat_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->h_shards) (void)hipHostFree(ctx->h_shards);
+    if (ctx->d_vmax) (void)hipFree(ctx->d_vmax);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -296,10 +305,10 @@ static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStre
 
 template <typename S>
 static hipError_t launch_build_ell(hipStream_t s, const slat_csr_view *B, uint32_t wq, uint32_t *ecol, void *eval,
-                                   uint8_t *eng) {
+                                   uint8_t *eng, unsigned long long *vmax, uint32_t epoch) {
     const uint64_t blocks = std::min<uint64_t>((B->n_rows + kBlock - 1) / kBlock, 4096);
     hipLaunchKernelGGL(k_build_ell<S>, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(kBlock), 0, s, B->row_ptr,
-                       B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng);
+                       B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng, vmax, epoch);
     return hipGetLastError();
 }
 
@@ -410,7 +419,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     Args asym = a;
     pick_window(ncols, kWave, 1984, asym.ww, asym.wide);
     pick_window(ncols, kWave, 1984, a.ww, a.wide);
-    a.cap = 448;  // 3 blocks of 4 waves per CU fit the 160 KB LDS at the 30^3 window (measured best)
+    a.area = 896 * 6;  // rank slots per wave: 896 narrow (u32 + u16) slots; 3 blocks/CU at the 30^3 window
     // padded ELL copy of B when its rows are short (bounded blow-up)
     const uint64_t wq = (maxrow_b + 3) / 4;
     const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
@@ -433,6 +442,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         a.ell_col = (const uint32_t *)(ws + o_ecol);
         a.ell_val = ws + o_eval;
         a.ell_ng = ws + o_eng;
+        if (dt == SLAT_U32) {
+            a.b_vmax = ctx->d_vmax;
+            a.epoch = ++ctx->epoch;
+        }
     }
     a.counts = (uint64_t *)ws;
     a.shards = (unsigned long long *)(ws + o_sh);
@@ -455,10 +468,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
 
     // LDS sizing and grid
-    const uint32_t vsz = dt == SLAT_SAT64 ? 16 : 8;  // LDS bytes per output slot
     const int wpb = kBlock / kWave;
-    if (const char *e_ = std::getenv("SLAT_CAP")) a.cap = std::max(64, std::atoi(e_));  // tuning knob
-    const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.cap, vsz).bytes;
+    if (const char *e_ = std::getenv("SLAT_CAP")) a.area = 6 * std::max(64, std::atoi(e_));  // tuning knob
+    a.area = (a.area + 15) & ~15u;
+    const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.area).bytes;
     if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
     const size_t sym_lds = (size_t)wpb * asym.ww * 4;
     const uint64_t max_blocks = (uint64_t)ctx->cu_count * 16;
@@ -477,11 +490,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (ell) {
         hipError_t be;
         if (dt == SLAT_U32)
-            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng);
+            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, ctx->d_vmax, a.epoch);
         else if (dt == SLAT_SAT64)
-            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng);
+            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, ctx->d_vmax, a.epoch);
         else
-            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng);
+            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, ctx->d_vmax, a.epoch);
         SLAT_HIP(ctx, be);
     }
     if (ablate & 7u) {

@@ -73,7 +73,7 @@ struct Args {
     uint64_t nrows, ncols;
     uint64_t b_nrows;  // column ids of A index rows of B: anything >= b_nrows is ignored
     uint32_t ww;     // bitmap words per window
-    uint32_t cap;    // rank-chunk capacity (value slots per LDS pass)
+    uint32_t area;   // LDS bytes per wave for rank slots (value + u16 column offset)
     uint32_t wide;   // 0 = one window at column 0 covers all columns; 1 = row-span windows
     uint32_t stats;  // count products into shard[3]
     uint32_t ell_wq; // groups of 4 per row in the padded ELL copy of B (0: CSR only)
@@ -81,6 +81,8 @@ struct Args {
     const uint32_t *ell_col;  // [n_B][ell_wq*4] columns, kSent padded
     const void *ell_val;      // [n_B][ell_wq*4] values
     const uint8_t *ell_ng;    // [n_B] groups of 4 holding real entries: ceil(len / 4)
+    unsigned long long *b_vmax;  // (epoch << 32) | max B value, from k_build_ell (u32 only; else null)
+    uint32_t epoch;
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
     uint32_t *c_col;
@@ -97,6 +99,7 @@ struct SemU32 {
     using V = unsigned long long;
     static constexpr int kSlots = 1;  // V words per output slot
     static constexpr bool kOrdered = false;
+    static constexpr bool kNarrowable = true;  // u32 slots when a row cannot overflow 2^32
     __device__ static __forceinline__ P prod(S a, S b) {
         const unsigned long long p = (unsigned long long)a * b;
         return p > 0xFFFFFFFFull ? 0xFFFFFFFFu : (P)p;  // Saturating<u32> product
@@ -116,6 +119,7 @@ struct SemSat64 {
     using V = unsigned long long;
     static constexpr int kSlots = 2;  // low / high 32-bit halves of the products, summed apart
     static constexpr bool kOrdered = false;
+    static constexpr bool kNarrowable = false;
     __device__ static __forceinline__ P prod(S a, S b) {
         return __umul64hi(a, b) != 0 ? ~0ull : a * b;  // Saturating<u64> product
     }
@@ -136,6 +140,7 @@ struct SemF64 {
     using V = double;
     static constexpr int kSlots = 1;
     static constexpr bool kOrdered = true;
+    static constexpr bool kNarrowable = false;
     __device__ static __forceinline__ P prod(S a, S b) { return __dmul_rn(a, b); }
     __device__ static __forceinline__ void acc(V *vals, uint32_t r, P p) {
         vals[r] = __dadd_rn(vals[r], p);  // no FMA contraction: Rust's a*b then +
@@ -273,7 +278,9 @@ __device__ __forceinline__ void row_span(const Args &p, I a0, I a1, uint64_t &lo
 // ------------------------------------------------------------------------------------------------
 template <typename S>
 __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const uint32_t *col, const S *val,
-                                                       uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng) {
+                                                       uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng,
+                                                       unsigned long long *vmax, uint32_t epoch) {
+    uint32_t mx = 0;
     for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kBlock) {
         const uint64_t s0 = rp[k], len = rp[k + 1] - s0;
         eng[k] = (uint8_t)((len + 3) / 4);
@@ -281,6 +288,20 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
             const uint64_t o = k * wq * 4 + u;
             ecol[o] = u < len ? col[s0 + u] : kSent;
             eval[o] = u < len ? val[s0 + u] : S(0);
+            if constexpr (std::is_same<S, uint32_t>::value)
+                if (u < len) mx = max(mx, (uint32_t)val[s0 + u]);
+        }
+    }
+    if constexpr (std::is_same<S, uint32_t>::value) {
+        // max B value, one atomic per block; the epoch in the high word supersedes earlier calls'
+        // values without a reset
+        __shared__ uint32_t bm[kBlock / kWave];
+        mx = wave_max_u32(mx);
+        if (lane_id() == 0) bm[threadIdx.x / kWave] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < kBlock / kWave; ++w) mx = max(mx, bm[w]);
+            atomicMax(vmax, ((unsigned long long)epoch << 32) | mx);
         }
     }
 }
@@ -465,17 +486,17 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
 // numeric: one wavefront per row
 // ------------------------------------------------------------------------------------------------
 struct NumLayout {
-    uint32_t off_vals, off_cols, bytes;
+    uint32_t off_slots, bytes;
 };
 
 // Per-wave LDS region: W ww*8 (uint2 per bitmap word: .x column bits, .y rank of the word's first
-// column, so a rank lookup is ONE ds_read_b64) | vals cap*slot_bytes | cols cap*4
-__host__ __device__ inline NumLayout num_layout(uint32_t ww, uint32_t cap, uint32_t slot_bytes) {
+// column, so a rank lookup is ONE ds_read_b64) | rank slots `area` bytes: values, then u16 column
+// offsets within the window
+__host__ __device__ inline NumLayout num_layout(uint32_t ww, uint32_t area) {
     auto up = [](uint32_t x, uint32_t a) { return (x + a - 1) / a * a; };
     NumLayout L;
-    L.off_vals = up(ww * 8, 16);
-    L.off_cols = up(L.off_vals + cap * slot_bytes, 16);
-    L.bytes = up(L.off_cols + cap * 4, 16);
+    L.off_slots = up(ww * 8, 16);
+    L.bytes = up(L.off_slots + area, 16);
     return L;
 }
 
@@ -629,13 +650,14 @@ struct BitmapPass {
     }
 };
 
-// numeric pass 3: accumulate products into rank slots; all rank lookups of a batch first
-template <typename Sem>
+// numeric pass 3: accumulate products into rank slots; all rank lookups of a batch first.
+// NARROW: u32 value slots (the row provably cannot reach 2^32), else the semiring's V slots.
+template <typename Sem, bool NARROW>
 struct AccPass {
     using S = typename Sem::S;
     const uint2 *W;
-    typename Sem::V *vals;
-    uint32_t *cols;
+    void *vals;
+    uint16_t *cols;  // column offset within the window
     uint32_t wlo, WIN, r0, nch;
     PhaseClock *pc;
     uint32_t abl;  // experiments: 64 no column stores, 128 no value atomics, 256 hashed ranks (no reads)
@@ -672,13 +694,17 @@ struct AccPass {
         }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const uint32_t cc[4] = {c[q].x, c[q].y, c[q].z, c[q].w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const uint32_t r = rank_in(w[q][e], off[q][e], ok[q][e], r0, nch);
                 if (r != kSent) {
-                    if (!(abl & 128u)) Sem::acc(vals, r, pr[q][e]);
-                    if (!(abl & 64u)) cols[r] = cc[e];
+                    if (!(abl & 128u)) {
+                        if constexpr (NARROW)
+                            atomicAdd((uint32_t *)vals + r, (uint32_t)pr[q][e]);
+                        else
+                            Sem::acc((typename Sem::V *)vals, r, pr[q][e]);
+                    }
+                    if (!(abl & 64u)) cols[r] = (uint16_t)off[q][e];
                 }
             }
         }
@@ -706,12 +732,19 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
 
     const int lane = lane_id();
     const int wv = threadIdx.x / kWave;
-    const NumLayout lay = num_layout(p.ww, p.cap, sizeof(V) * Sem::kSlots);
+    const NumLayout lay = num_layout(p.ww, p.area);
     uint8_t *region = smem8 + (size_t)wv * lay.bytes;
     uint2 *W = (uint2 *)region;
     uint32_t *L0 = (uint32_t *)region;  // L0[2w] aliases W[w].x
-    V *vals = (V *)(region + lay.off_vals);
-    uint32_t *cols = (uint32_t *)(region + lay.off_cols);
+    uint8_t *slots = region + lay.off_slots;
+    // rank-chunk capacities: narrow = u32 value + u16 column, wide = V*kSlots + u16 column
+    const uint32_t cap_n = p.area / 6, cap_w = p.area / (uint32_t)(sizeof(V) * Sem::kSlots + 2);
+    uint32_t bvmax = 0xFFFFFFFFu;  // max B value of this call (u32 semiring with the ELL copy)
+    if constexpr (Sem::kNarrowable)
+        if (p.b_vmax) {
+            const unsigned long long v = *(volatile unsigned long long *)p.b_vmax;
+            if ((uint32_t)(v >> 32) == p.epoch) bvmax = (uint32_t)v;
+        }
     S *cval = (S *)p.c_val;
     const S *av_ = (const S *)p.a_val;
 
@@ -749,6 +782,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
             S aq[kRegQ];
             uint32_t bk0 = kSent, bk1 = kSent, bt0 = 0, bt1 = 0, nb = 0;
             S ba0 = S(0), ba1 = S(0);
+            uint32_t amax = 0;  // lane max of the A values seen (narrow-slot bound)
             auto load_seg = [&](I sb) {
                 // bare loads inside the branches, all arithmetic on them after: a use inside the
                 // branch would make the wave wait there, serialising the q loads
@@ -764,6 +798,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 });
                 sfor<kRegQ>([&](auto Q) {
                     if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
+                    if constexpr (Sem::kNarrowable) amax = max(amax, (uint32_t)aq[Q]);
                 });
                 if constexpr (!ELL) return;
                 uint32_t mx = 0;
@@ -893,43 +928,72 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                     }
                 }
                 mark(2);  // word ranks
-                for (uint32_t r0 = 0; r0 < wcnt; r0 += p.cap) {
-                    const uint32_t nch = min(p.cap, wcnt - r0);
-                    for (uint32_t t = lane; t < nch * Sem::kSlots; t += kWave) vals[t] = V(0);
-                    wave_sync();
-                    mark(8);  // zero value slots
-                    // 3. values and the column of every rank (duplicates store the same column)
-                    if constexpr (Sem::kOrdered) {
-                        if (!(p.ablate & 8u))
-                            traverse_ordered<I, S>(p, a0, a1, [&](uint32_t j, S a, S b) {
-                                uint32_t off;
-                                bool ok;
-                                const uint2 w = rank_word(W, j, wlo, WIN, off, ok);
-                                const uint32_t r = rank_in(w, off, ok, r0, nch);
-                                if (r != kSent) {
-                                    Sem::acc(vals, r, Sem::prod(a, b));
-                                    cols[r] = j;
-                                }
-                            });
-                    } else if (!(p.ablate & 8u)) {
-                        AccPass<Sem> acc{W, vals, cols, wlo, WIN, r0, nch, &pc, p.ablate};
-                        each_group(acc, std::true_type{});
+                // narrow u32 slots when the row's sums provably stay below 2^32:
+                // max(A row) * max(B) * len(A row) < 2^32 (each output sums <= len products)
+                bool narrow = false;
+                if constexpr (Sem::kNarrowable) {
+                    if (ELL && bvmax != 0xFFFFFFFFu) {
+                        const uint64_t x = (uint64_t)wave_max_u32(amax) * bvmax;
+                        narrow = x == 0 || len <= 0xFFFFFFFFull / x;
                     }
-                    wave_sync();
-                    if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
-                    mark(12);  // accumulate pass drain
-                    // 4. emit at the row's slice, coalesced
-                    for (uint32_t t = lane; t < nch; t += kWave) {
-                        const S v = Sem::finish(vals, t);
-                        zeros += Sem::is_zero(v) ? 1u : 0u;
-                        if (out_pos + t < out_end && !(p.ablate & 16u)) {  // never trust blindly
-                            p.c_col[out_pos + t] = cols[t];
-                            cval[out_pos + t] = v;
+                }
+                auto run_chunks = [&](auto narrow_tag) {
+                    constexpr bool NW = decltype(narrow_tag)::value;
+                    using VS = std::conditional_t<NW, uint32_t, V>;  // value slot word
+                    constexpr uint32_t kVW = NW ? 1 : Sem::kSlots;   // words per slot
+                    const uint32_t cap = NW ? cap_n : cap_w;
+                    VS *vals = (VS *)slots;
+                    uint16_t *cols = (uint16_t *)(slots + ((cap * kVW * sizeof(VS) + 3) & ~3u));
+                    for (uint32_t r0 = 0; r0 < wcnt; r0 += cap) {
+                        const uint32_t nch = min(cap, wcnt - r0);
+                        for (uint32_t t = lane; t < nch * kVW; t += kWave) vals[t] = VS(0);
+                        wave_sync();
+                        mark(8);  // zero value slots
+                        // 3. values and the column offset of every rank (duplicates store the same)
+                        if constexpr (Sem::kOrdered) {
+                            if (!(p.ablate & 8u))
+                                traverse_ordered<I, S>(p, a0, a1, [&](uint32_t j, S a, S b) {
+                                    uint32_t off;
+                                    bool ok;
+                                    const uint2 w = rank_word(W, j, wlo, WIN, off, ok);
+                                    const uint32_t r = rank_in(w, off, ok, r0, nch);
+                                    if (r != kSent) {
+                                        Sem::acc((V *)vals, r, Sem::prod(a, b));
+                                        cols[r] = (uint16_t)off;
+                                    }
+                                });
+                        } else if (!(p.ablate & 8u)) {
+                            AccPass<Sem, NW> acc{W, vals, cols, wlo, WIN, r0, nch, &pc, p.ablate};
+                            each_group(acc, std::true_type{});
                         }
+                        wave_sync();
+                        if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
+                        mark(12);  // accumulate pass drain
+                        // 4. emit at the row's slice, coalesced
+                        for (uint32_t t = lane; t < nch; t += kWave) {
+                            S v;
+                            if constexpr (NW)
+                                v = (S)vals[t];
+                            else
+                                v = Sem::finish((const V *)vals, t);
+                            zeros += Sem::is_zero(v) ? 1u : 0u;
+                            if (out_pos + t < out_end && !(p.ablate & 16u)) {  // never trust blindly
+                                p.c_col[out_pos + t] = wlo + cols[t];
+                                cval[out_pos + t] = v;
+                            }
+                        }
+                        out_pos += nch;
+                        wave_sync();
+                        mark(4);  // emit
                     }
-                    out_pos += nch;
-                    wave_sync();
-                    mark(4);  // emit
+                };
+                if constexpr (Sem::kNarrowable) {
+                    if (narrow)
+                        run_chunks(std::true_type{});
+                    else
+                        run_chunks(std::false_type{});
+                } else {
+                    run_chunks(std::false_type{});
                 }
                 for (uint32_t q = 0; q < per; ++q) W[wb0 + q].x = 0;
                 wave_sync();

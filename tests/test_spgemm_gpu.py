@@ -134,6 +134,25 @@ def test_large_values_saturate_u32_products(ctx):
     assert_same(to_dev(o, slat.SAT64)._spgemm(to_dev(o, slat.SAT64)), O.matmul_seq(o, o), "sat64")
 
 
+@pytest.mark.parametrize("k", [3, 4, 5])
+def test_u32_narrow_slot_bound(ctx, k):
+    # The kernel accumulates a row in u32 slots only when max(A row) * max(B) * len(A row) < 2^32,
+    # else in u64 slots. Row 0 has k entries of 2^30 that all hit column 0 of B (value 1):
+    # k = 3 -> narrow (sum 3 * 2^30), k = 4 -> wide (sum 2^32 saturates), k = 5 -> wide (saturates).
+    n = 64
+    r = np.concatenate([np.zeros(k, np.int64), np.arange(1, n)])
+    c = np.concatenate([np.arange(1, k + 1), np.arange(1, n)])
+    v = np.concatenate([np.full(k, 1 << 30), np.full(n - 1, 7)]).astype(np.uint64)
+    a = O.from_coo(n, r, c, v, O.U32)
+    br = np.concatenate([np.arange(1, k + 1), np.arange(n)])
+    bc = np.concatenate([np.zeros(k, np.int64), (np.arange(n) * 7) % n])
+    b = O.from_coo(n, br, bc, np.ones(len(br), np.uint64), O.U32)
+    want = O.matmul_seq(a, b)
+    assert_same(to_dev(a, slat.U32)._spgemm(to_dev(b, slat.U32)), want, f"narrow bound k={k}")
+    if k >= 4:
+        assert want.get(0, 0) == 0xFFFFFFFF
+
+
 # ---- f64 (config C5 shape, small): bit-exact left fold ----
 def test_f64_rmat_bit_exact(ctx):
     h = slat.host_rmat(12, 40000)
