@@ -245,30 +245,6 @@ __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&
     }
 }
 
-// Column span [lo, hi] of row i of A·B from B's row ends (B rows are sorted); lo > hi if empty.
-template <typename I>
-__device__ __forceinline__ void row_span(const Args &p, I a0, I a1, uint64_t &lo, uint64_t &hi) {
-    const int lane = lane_id();
-    uint32_t l = 0xFFFFFFFFu, h = 0;
-    for (I idx = a0 + (I)lane; idx < a1; idx += (I)kWave) {
-        const uint32_t k = p.a_col[idx];
-        if (k >= p.b_nrows) continue;
-        const I bs = (I)p.b_rp[k], be = (I)p.b_rp[k + 1];
-        if (be > bs) {
-            l = min(l, p.b_col[bs]);
-            h = max(h, p.b_col[be - 1]);
-        }
-    }
-    l = wave_min_u32(l);
-    h = wave_max_u32(h);
-    lo = l;
-    hi = h;
-    if (l > h) {
-        lo = 1;
-        hi = 0;
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // padded ELL copy of B (rows of B short, e.g. the base adjacency of an A^k chain): row k holds
 // ell_wq groups of 4 columns at ell_col[k*ell_wq ..], padded with kSent, and the matching values
@@ -359,6 +335,7 @@ __device__ __forceinline__ Quad<typename Sem::S> prods(typename Sem::S a, const 
 // passes that need no values (symbolic, bitmap, column span) walk with this stand-in semiring
 struct SemNone {
     using S = uint32_t;
+    static constexpr bool kNarrowable = false;
     __device__ static __forceinline__ S prod(S, S) { return 0; }
 };
 
@@ -412,75 +389,7 @@ __device__ __forceinline__ bool win_off(uint32_t c, uint32_t wlo, uint32_t WIN, 
     return c != kSent && off < WIN;
 }
 
-// atomicOr the (up to) four columns of a group into the window bitmap; no returned values
-__device__ __forceinline__ void bitmap_or4(uint32_t *L0, uint4 c, uint32_t wlo, uint32_t WIN) {
-    const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        uint32_t off;
-        if (win_off(cc[e], wlo, WIN, off)) atomicOr(&L0[off >> 5], 1u << (off & 31));
-    }
-}
 
-// ------------------------------------------------------------------------------------------------
-// symbolic: structural nnz per output row, one wavefront per row
-// ------------------------------------------------------------------------------------------------
-template <typename I, bool ELL>
-__global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    constexpr int kWpb = kBlock / kWave;
-    const int lane = lane_id();
-    const int wv = threadIdx.x / kWave;
-    uint32_t *L0 = smem + (size_t)wv * p.ww;
-    if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) p.c_rp[0] = 0;
-        if (threadIdx.x < kShards) {  // fields read by k_numeric; [3] (flops) is zeroed by the host
-            p.shards[threadIdx.x * kShardStride + 1] = 0;
-            p.shards[threadIdx.x * kShardStride + 2] = 0;
-        }
-    }
-    for (uint32_t w = lane; w < p.ww; w += kWave) L0[w] = 0;
-    wave_sync();
-    const uint32_t WIN = p.ww * 32;
-    const uint32_t per = p.ww / kWave;  // odd: lane-contiguous word ownership is conflict-free
-    const uint32_t wb0 = lane * per;
-    unsigned long long flops = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * kWpb;
-    for (uint64_t row = (uint64_t)blockIdx.x * kWpb + wv; row < p.nrows; row += stride) {
-        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
-        uint64_t cnt = 0;
-        if (a1 > a0) {
-            uint64_t lo = 0, hi = p.ncols - 1;
-            if (p.wide) row_span<I>(p, a0, a1, lo, hi);
-            bool first = true;
-            for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) {
-                uint32_t nprod = 0, x = 0;
-                walk_row<SemNone, ELL, false, I>(p, a0, a1, [&](uint4 c, const Quad<uint32_t> &) {
-                    if (p.stats) nprod += (c.x != kSent) + (c.y != kSent) + (c.z != kSent) + (c.w != kSent);
-                    if (p.ablate & 1u)
-                        x ^= c.x ^ c.y ^ c.z ^ c.w;
-                    else
-                        bitmap_or4(L0, c, (uint32_t)wlo, WIN);
-                });
-                wave_sync();
-                // count = popcount of the window; lane owns words [wb0, wb0 + per) and clears them
-                uint32_t lc = 0;
-                for (uint32_t q = 0; q < per; ++q) {
-                    lc += __popc(L0[wb0 + q]);
-                    L0[wb0 + q] = 0;
-                }
-                if (p.ablate & 1u) lc += x & 1u;
-                cnt += wave_sum_u32(lc);
-                if (p.stats && first) flops += wave_sum_u32(nprod);
-                first = false;
-                wave_sync();
-            }
-        }
-        if (lane == 0) p.counts[row] = cnt;
-    }
-    if (p.stats && lane == 0 && flops)
-        atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
-}
 
 // ------------------------------------------------------------------------------------------------
 // numeric: one wavefront per row
@@ -614,6 +523,150 @@ __device__ __forceinline__ uint32_t for_tails(const Args &p, const uint32_t *kq,
     return bi;
 }
 
+// ------------------------------------------------------------------------------------------------
+// RowWalker: every group (4 B entries as columns + products) of one row of A·B, for one wave.
+// A entries are taken in segments of 64*kRegQ held by the lanes (kq/aq). With the ELL copy of B,
+// a segment's later groups (entry, t >= 1) of ALL rounds are compacted with ds_permute into at
+// most kNB dense 64-lane batches of (B row, group, a) kept in registers, so a pass issues all of a
+// segment's group loads at once (one L2 round trip) and masked-off lanes do not burn LDS
+// instructions. One-segment rows keep their segment across passes; longer rows rebuild it per pass.
+// Loads sit bare inside their branches and all arithmetic on them comes after: a use inside the
+// branch would make the wave wait there and serialise the loads.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kNB = 2;  // compacted tail batches per segment (bk0/bk1)
+
+template <typename Sem, typename I, bool ELL, bool AVALS>
+struct RowWalker {
+    using S = typename Sem::S;
+    static constexpr uint32_t kSeg = kWave * kRegQ;
+    static constexpr uint32_t kOvf = 0xFFFFFFFFu;  // segment with more tail items than kNB batches
+    const Args &p;
+    I a0, a1;
+    uint64_t len;
+    uint32_t nseg;
+    bool single;
+    uint32_t kq[kRegQ], ngq[kRegQ];
+    S aq[kRegQ];
+    uint32_t bk0 = kSent, bk1 = kSent, bt0 = 0, bt1 = 0, nb = 0;
+    S ba0 = S(0), ba1 = S(0);
+    uint32_t amax = 0;  // lane max of the A values seen (narrow-slot bound, u32)
+
+    __device__ __forceinline__ RowWalker(const Args &p_, I a0_, I a1_) : p(p_), a0(a0_), a1(a1_) {
+        len = (uint64_t)(a1 - a0);
+        nseg = (uint32_t)((len + kSeg - 1) / kSeg);
+        single = nseg == 1;
+        if (single) load_seg(a0);
+    }
+
+    __device__ __forceinline__ void load_seg(I sb) {
+        const int lane = lane_id();
+        const S *av_ = (const S *)p.a_val;
+        sfor<kRegQ>([&](auto Q) {
+            constexpr int q = Q;
+            const I idx = sb + (I)(q * kWave + lane);
+            kq[q] = kSent;
+            aq[q] = S(0);
+            if (idx < a1) {
+                kq[q] = p.a_col[idx];
+                if constexpr (AVALS) aq[q] = av_[idx];
+            }
+        });
+        sfor<kRegQ>([&](auto Q) {
+            if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
+            if constexpr (Sem::kNarrowable) amax = max(amax, (uint32_t)aq[Q]);
+        });
+        if constexpr (!ELL) return;
+        uint32_t mx = 0;
+        sfor<kRegQ>([&](auto Q) {
+            constexpr int q = Q;
+            ngq[q] = kq[q] != kSent ? p.ell_ng[kq[q]] : 0u;
+            mx = max(mx, ngq[q]);
+        });
+        mx = wave_max_u32(mx);
+        bk0 = bk1 = kSent;
+        uint32_t off = 0;  // items placed so far (uniform)
+        for (uint32_t t = 1; t < mx; ++t) {
+            sfor<kRegQ>([&](auto Q) {
+                constexpr int q = Q;
+                const bool has = ngq[q] > t;
+                const unsigned long long m = __ballot(has);
+                const uint32_t cnt = __popcll(m);
+                if (cnt == 0) return;
+                const uint32_t below =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                // senders go to lanes (off + rank) mod 64; the rest to a lane outside that range
+                // (one exists unless all 64 lanes send)
+                const int dst = (int)(((has ? off + below : off + cnt) & (kWave - 1)) * 4);
+                const uint32_t rk = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)kq[q]);
+                const S ra = AVALS ? permute_val(dst, aq[q]) : S(0);
+                const uint32_t i = ((uint32_t)lane - off) & (kWave - 1);  // receive slot
+                const uint32_t g = off + i;                              // item index -> batch g / 64
+                // value selects, not conditional stores: keeps the batch registers in VGPRs
+                const bool in0 = (i < cnt) & (g < (uint32_t)kWave);
+                const bool in1 = (i < cnt) & (g >= (uint32_t)kWave) & (g < 2u * kWave);
+                bk0 = in0 ? rk : bk0;
+                ba0 = in0 ? ra : ba0;
+                bt0 = in0 ? t : bt0;
+                bk1 = in1 ? rk : bk1;
+                ba1 = in1 ? ra : ba1;
+                bt1 = in1 ? t : bt1;
+                off += cnt;
+            });
+        }
+        nb = (off + kWave - 1) / kWave;
+        if (nb > kNB) nb = kOvf;
+    }
+
+    // grp(c4, pr4) / grp.multi(c4[kRegQ], pr4[kRegQ]) for every group; products when VV
+    template <bool VV, typename G>
+    __device__ __forceinline__ void each_group(G &grp) {
+        if constexpr (ELL) {
+            for (uint32_t sg = 0; sg < nseg; ++sg) {
+                if (!single) load_seg(a0 + (I)((uint64_t)sg * kSeg));
+                if (nb == kOvf) {  // rare: too many tail items for the register batches
+                    sfor<kRegQ>([&](auto Q) {
+                        if (kq[Q] != kSent) walk_brow<Sem, true, VV, I>(p, kq[Q], aq[Q], 0, grp);
+                    });
+                    continue;
+                }
+                uint4 cq[kRegQ], ct0 = make_uint4(kSent, kSent, kSent, kSent), ct1 = ct0;
+                Quad<S> pq[kRegQ], pt0{}, pt1{};
+                sfor<kRegQ>([&](auto Q) {
+                    constexpr int q = Q;
+                    cq[q] = make_uint4(kSent, kSent, kSent, kSent);
+                    pq[q] = Quad<S>{};
+                    if (kq[q] != kSent) {
+                        cq[q] = ell_cols(p, kq[q], 0);
+                        if constexpr (VV) pq[q] = ell_vals<S>(p, kq[q], 0);
+                    }
+                });
+                if (bk0 != kSent) {
+                    ct0 = ell_cols(p, bk0, bt0);
+                    if constexpr (VV) pt0 = ell_vals<S>(p, bk0, bt0);
+                }
+                if (bk1 != kSent) {
+                    ct1 = ell_cols(p, bk1, bt1);
+                    if constexpr (VV) pt1 = ell_vals<S>(p, bk1, bt1);
+                }
+                if constexpr (VV) {
+                    sfor<kRegQ>([&](auto Q) { pq[Q] = prods<Sem>(aq[Q], pq[Q]); });
+                    pt0 = prods<Sem>(ba0, pt0);
+                    pt1 = prods<Sem>(ba1, pt1);
+                }
+                grp.multi(cq, pq);
+                if (nb > 0) grp(ct0, pt0);
+                if (nb > 1) grp(ct1, pt1);
+            }
+        } else if (single) {
+            sfor<kRegQ>([&](auto Q) {
+                if (kq[Q] != kSent) walk_brow<Sem, false, VV, I>(p, kq[Q], aq[Q], 0, grp);
+            });
+        } else {
+            walk_row<Sem, false, VV, I>(p, a0, a1, grp);
+        }
+    }
+};
+
 // numeric pass 1: column span of the row (rows wider than one window)
 template <typename S>
 struct SpanPass {
@@ -632,17 +685,18 @@ struct SpanPass {
     }
 };
 
-// numeric pass 2: the window's column bitmap (W[w].x), fire-and-forget LDS atomics
-template <typename S>
+// the window's column bitmap: word w at L0[w * STRIDE] (numeric: W[w].x, STRIDE 2; symbolic: 1),
+// fire-and-forget LDS atomics
+template <typename S, int STRIDE = 2>
 struct BitmapPass {
-    uint32_t *L0;  // L0[2w] aliases W[w].x
+    uint32_t *L0;
     uint32_t wlo, WIN;
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &) {
         const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             uint32_t off;
-            if (win_off(cc[e], wlo, WIN, off)) atomicOr(&L0[(off >> 5) * 2], 1u << (off & 31));
+            if (win_off(cc[e], wlo, WIN, off)) atomicOr(&L0[(off >> 5) * STRIDE], 1u << (off & 31));
         }
     }
     __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
@@ -716,10 +770,88 @@ struct AccPass {
     }
 };
 
+// ------------------------------------------------------------------------------------------------
+// symbolic: structural nnz per output row, one wavefront per row (the RowWalker traversal, column
+// bitmap only; counts = popcounts of the lane-owned words, which the same lanes then clear)
+// ------------------------------------------------------------------------------------------------
+template <int STRIDE>
+struct SymPass {
+    BitmapPass<uint32_t, STRIDE> bm;
+    bool count;
+    uint32_t nprod = 0;
+    __device__ __forceinline__ void operator()(uint4 c, const Quad<uint32_t> &pr) {
+        bm(c, pr);
+        if (count) nprod += (c.x != kSent) + (c.y != kSent) + (c.z != kSent) + (c.w != kSent);
+    }
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<uint32_t> *pr) {
+        sfor<kRegQ>([&](auto Q) { (*this)(c[Q], pr[Q]); });
+    }
+};
+
+template <typename I, bool ELL>
+__global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    constexpr int kWpb = kBlock / kWave;
+    const int lane = lane_id();
+    const int wv = threadIdx.x / kWave;
+    uint32_t *L0 = smem + (size_t)wv * p.ww;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) p.c_rp[0] = 0;
+        if (threadIdx.x < kShards) {  // fields read by k_numeric; [3] (flops) is zeroed by the host
+            p.shards[threadIdx.x * kShardStride + 1] = 0;
+            p.shards[threadIdx.x * kShardStride + 2] = 0;
+        }
+    }
+    for (uint32_t w = lane; w < p.ww; w += kWave) L0[w] = 0;
+    wave_sync();
+    const uint32_t WIN = p.ww * 32;
+    const uint32_t per = p.ww / kWave;  // odd: lane-contiguous word ownership is conflict-free
+    const uint32_t wb0 = lane * per;
+    unsigned long long flops = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kWpb;
+    for (uint64_t row = (uint64_t)blockIdx.x * kWpb + wv; row < p.nrows; row += stride) {
+        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
+        uint64_t cnt = 0;
+        if (a1 > a0) {
+            RowWalker<SemNone, I, ELL, false> rw(p, a0, a1);
+            uint64_t lo = 0, hi = p.ncols - 1;
+            if (p.wide) {
+                SpanPass<uint32_t> mm;
+                rw.template each_group<false>(mm);
+                const uint32_t l = wave_min_u32(mm.l), h = wave_max_u32(mm.h);
+                lo = l;
+                hi = h;
+                if (l > h) {
+                    lo = 1;
+                    hi = 0;
+                }
+            }
+            bool first = true;
+            for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) {
+                SymPass<1> sp{BitmapPass<uint32_t, 1>{L0, (uint32_t)wlo, WIN}, p.stats != 0 && first};
+                if (!(p.ablate & 1u)) rw.template each_group<false>(sp);
+                wave_sync();
+                // count = popcount of the window; lane owns words [wb0, wb0 + per) and clears them
+                uint32_t lc = 0;
+                for (uint32_t q = 0; q < per; ++q) {
+                    lc += __popc(L0[wb0 + q]);
+                    L0[wb0 + q] = 0;
+                }
+                cnt += wave_sum_u32(lc);
+                if (first && p.stats) flops += wave_sum_u32(sp.nprod);
+                first = false;
+                wave_sync();
+            }
+        }
+        if (lane == 0) p.counts[row] = cnt;
+    }
+    if (p.stats && lane == 0 && flops)
+        atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
+}
+
 #ifndef SLAT_NUM_ATTR
 #define SLAT_NUM_ATTR
 #endif
-constexpr uint32_t kNB = 2;  // compacted tail batches kept in registers per row (ct0/ct1)
 
 template <typename Sem, typename I, bool ELL>
 __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
@@ -746,7 +878,6 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
             if ((uint32_t)(v >> 32) == p.epoch) bvmax = (uint32_t)v;
         }
     S *cval = (S *)p.c_val;
-    const S *av_ = (const S *)p.a_val;
 
     if (blockIdx.x == 0 && threadIdx.x == 0) p.shards[0] = p.c_rp[p.nrows];
     for (uint32_t w = lane; w < p.ww; w += kWave) W[w] = make_uint2(0u, 0u);
@@ -768,132 +899,11 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
         uint32_t zeros = 0;
         ph[kPhaseSlots - 1] += 1;
         if (a1 > a0) {
-            // A entries are taken in segments of 64*kRegQ held by the lanes (kq/aq). With the ELL
-            // copy of B, a segment's later groups (entry, t >= 1) of ALL rounds are compacted into at
-            // most kNB dense 64-lane batches of (B row, group, a) in registers, so a pass issues all
-            // of a segment's group loads at once (one L2 round trip). One-segment rows keep their
-            // segment across passes; longer rows rebuild it per pass.
-            constexpr uint32_t kSeg = kWave * kRegQ;
-            constexpr uint32_t kOvf = 0xFFFFFFFFu;  // segment with more tail items than kNB batches
-            const uint64_t len = (uint64_t)(a1 - a0);
-            const uint32_t nseg = (uint32_t)((len + kSeg - 1) / kSeg);
-            const bool single = nseg == 1;
-            uint32_t kq[kRegQ], ngq[kRegQ];
-            S aq[kRegQ];
-            uint32_t bk0 = kSent, bk1 = kSent, bt0 = 0, bt1 = 0, nb = 0;
-            S ba0 = S(0), ba1 = S(0);
-            uint32_t amax = 0;  // lane max of the A values seen (narrow-slot bound)
-            auto load_seg = [&](I sb) {
-                // bare loads inside the branches, all arithmetic on them after: a use inside the
-                // branch would make the wave wait there, serialising the q loads
-                sfor<kRegQ>([&](auto Q) {
-                    constexpr int q = Q;
-                    const I idx = sb + (I)(q * kWave + lane);
-                    kq[q] = kSent;
-                    aq[q] = S(0);
-                    if (idx < a1) {
-                        kq[q] = p.a_col[idx];
-                        if constexpr (kVals) aq[q] = av_[idx];
-                    }
-                });
-                sfor<kRegQ>([&](auto Q) {
-                    if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
-                    if constexpr (Sem::kNarrowable) amax = max(amax, (uint32_t)aq[Q]);
-                });
-                if constexpr (!ELL) return;
-                uint32_t mx = 0;
-                sfor<kRegQ>([&](auto Q) {
-                    constexpr int q = Q;
-                    ngq[q] = kq[q] != kSent ? p.ell_ng[kq[q]] : 0u;
-                    mx = max(mx, ngq[q]);
-                });
-                mx = wave_max_u32(mx);
-                bk0 = bk1 = kSent;
-                uint32_t off = 0;  // items placed so far (uniform)
-                for (uint32_t t = 1; t < mx; ++t) {
-                    sfor<kRegQ>([&](auto Q) {
-                        constexpr int q = Q;
-                        const bool has = ngq[q] > t;
-                        const unsigned long long m = __ballot(has);
-                        const uint32_t cnt = __popcll(m);
-                        if (cnt == 0) return;
-                        const uint32_t below =
-                            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        // senders go to lanes (off + rank) mod 64; the rest to a lane outside that
-                        // range (one exists unless all 64 lanes send)
-                        const int dst = (int)(((has ? off + below : off + cnt) & (kWave - 1)) * 4);
-                        const uint32_t rk = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)kq[q]);
-                        const S ra = permute_val(dst, aq[q]);
-                        const uint32_t i = ((uint32_t)lane - off) & (kWave - 1);  // receive slot
-                        const uint32_t g = off + i;  // global item index -> batch g / 64
-                        // value selects, not conditional stores: keeps the batch registers in VGPRs
-                        const bool in0 = (i < cnt) & (g < (uint32_t)kWave);
-                        const bool in1 = (i < cnt) & (g >= (uint32_t)kWave) & (g < 2u * kWave);
-                        bk0 = in0 ? rk : bk0;
-                        ba0 = in0 ? ra : ba0;
-                        bt0 = in0 ? t : bt0;
-                        bk1 = in1 ? rk : bk1;
-                        ba1 = in1 ? ra : ba1;
-                        bt1 = in1 ? t : bt1;
-                        off += cnt;
-                    });
-                }
-                nb = (off + kWave - 1) / kWave;
-                if (nb > kNB) nb = kOvf;
-            };
-            if (single) load_seg(a0);
-            if constexpr (SLAT_PHASES) pin(kq[0]);  // wait for the A entries inside phase 0
+            RowWalker<Sem, I, ELL, kVals> rw(p, a0, a1);
+            const uint64_t len = rw.len;
+            if constexpr (SLAT_PHASES) pin(rw.kq[0]);  // wait for the A entries inside phase 0
             mark(0);  // row bounds + A entries, group counts, tail compaction
-            // every group of the row, as (columns, products)
-            auto each_group = [&](auto &&grp, auto vals_tag) {
-                constexpr bool VV = decltype(vals_tag)::value;
-                if constexpr (ELL) {
-                    for (uint32_t sg = 0; sg < nseg; ++sg) {
-                        if (!single) load_seg(a0 + (I)((uint64_t)sg * kSeg));
-                        if (nb == kOvf) {  // rare: too many tail items for the register batches
-                            sfor<kRegQ>([&](auto Q) {
-                                if (kq[Q] != kSent) walk_brow<Sem, true, VV, I>(p, kq[Q], aq[Q], 0, grp);
-                            });
-                            continue;
-                        }
-                        // every load of the segment issued before any is used (bare loads in the
-                        // branches; products computed after, unconditionally)
-                        uint4 cq[kRegQ], ct0 = make_uint4(kSent, kSent, kSent, kSent), ct1 = ct0;
-                        Quad<S> pq[kRegQ], pt0{}, pt1{};
-                        sfor<kRegQ>([&](auto Q) {
-                            constexpr int q = Q;
-                            cq[q] = make_uint4(kSent, kSent, kSent, kSent);
-                            pq[q] = Quad<S>{};
-                            if (kq[q] != kSent) {
-                                cq[q] = ell_cols(p, kq[q], 0);
-                                if constexpr (VV) pq[q] = ell_vals<S>(p, kq[q], 0);
-                            }
-                        });
-                        if (bk0 != kSent) {
-                            ct0 = ell_cols(p, bk0, bt0);
-                            if constexpr (VV) pt0 = ell_vals<S>(p, bk0, bt0);
-                        }
-                        if (bk1 != kSent) {
-                            ct1 = ell_cols(p, bk1, bt1);
-                            if constexpr (VV) pt1 = ell_vals<S>(p, bk1, bt1);
-                        }
-                        if constexpr (VV) {
-                            sfor<kRegQ>([&](auto Q) { pq[Q] = prods<Sem>(aq[Q], pq[Q]); });
-                            pt0 = prods<Sem>(ba0, pt0);
-                            pt1 = prods<Sem>(ba1, pt1);
-                        }
-                        grp.multi(cq, pq);
-                        if (nb > 0) grp(ct0, pt0);
-                        if (nb > 1) grp(ct1, pt1);
-                    }
-                } else if (single) {
-                    sfor<kRegQ>([&](auto Q) {
-                        if (kq[Q] != kSent) walk_brow<Sem, false, VV, I>(p, kq[Q], aq[Q], 0, grp);
-                    });
-                } else {
-                    walk_row<Sem, false, VV, I>(p, a0, a1, grp);
-                }
-            };
+            auto each_group = [&](auto &&grp, auto vals_tag) { rw.template each_group<decltype(vals_tag)::value>(grp); };
             uint64_t lo = 0, hi = p.ncols - 1;
             if (p.wide) {
                 SpanPass<S> mm;
@@ -933,7 +943,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 bool narrow = false;
                 if constexpr (Sem::kNarrowable) {
                     if (ELL && bvmax != 0xFFFFFFFFu) {
-                        const uint64_t x = (uint64_t)wave_max_u32(amax) * bvmax;
+                        const uint64_t x = (uint64_t)wave_max_u32(rw.amax) * bvmax;
                         narrow = x == 0 || len <= 0xFFFFFFFFull / x;
                     }
                 }
