@@ -64,7 +64,9 @@ typedef struct {
     uint64_t max_row_nnz;
 } slat_csr_view;
 
-/* Library-owned device CSR. capacity >= nnz entries are allocated for col_idx/values. */
+/* Library-owned device CSR. capacity >= nnz entries are allocated for col_idx/values. `alloc` is
+ * private to the library (how the arrays were allocated: one block or several); treat the whole
+ * struct as read-only and release it with slat_csr_free. */
 typedef struct {
     uint64_t n_rows, n_cols, nnz, capacity, max_row_nnz;
     uint64_t *row_ptr;
@@ -72,6 +74,8 @@ typedef struct {
     void *values;
     int32_t dtype;
     int32_t device;
+    int32_t alloc;
+    int32_t _pad;
 } slat_csr;
 
 typedef struct {

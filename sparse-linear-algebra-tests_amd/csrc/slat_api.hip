@@ -33,7 +33,7 @@ struct slat_ctx {
     // workspace (grown on demand)
     void *ws = nullptr;
     size_t ws_bytes = 0;
-    unsigned long long *h_shards = nullptr;  // pinned
+    unsigned long long *h_shards = nullptr;  // pinned, mapped
     unsigned long long *d_vmax = nullptr;    // (epoch << 32) | max B value, written by k_build_ell
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
     hipEvent_t ev[6] = {};
@@ -55,6 +55,22 @@ static slat_status fail(slat_ctx *ctx, slat_status s, const std::string &msg) {
 }
 
 static size_t vsize(int32_t dtype) { return dtype == SLAT_U32 ? 4 : 8; }
+
+// C arrays in one stream-ordered pool block (one malloc, one free per matrix):
+// row_ptr | col_idx | values, each 256-byte aligned. alloc = 1 marks the layout for slat_csr_free.
+enum { kAllocSeparate = 0, kAllocJoint = 1 };
+static hipError_t alloc_joint(slat_csr *m, uint64_t nrows, uint64_t cap, size_t vs, hipStream_t s) {
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t rp_b = up((nrows + 1) * 8), col_b = up(std::max<uint64_t>(cap, 1) * 4);
+    uint8_t *base = nullptr;
+    const hipError_t e = hipMallocAsync((void **)&base, rp_b + col_b + std::max<uint64_t>(cap, 1) * vs, s);
+    if (e != hipSuccess) return e;
+    m->row_ptr = (uint64_t *)base;
+    m->col_idx = (uint32_t *)(base + rp_b);
+    m->values = base + rp_b + col_b;
+    m->alloc = kAllocJoint;
+    return hipSuccess;
+}
 
 extern "C" {
 
@@ -101,7 +117,7 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         delete ctx;
         return SLAT_EOOM;
     }
-    if (hipMalloc((void **)&ctx->d_vmax, 8) != hipSuccess || hipMemset(ctx->d_vmax, 0, 8) != hipSuccess) {
+    if (hipMalloc((void **)&ctx->d_vmax, 16) != hipSuccess || hipMemset(ctx->d_vmax, 0, 16) != hipSuccess) {
         (void)hipHostFree(ctx->h_shards);
         (void)hipStreamDestroy(ctx->own_stream);
         delete ctx;
@@ -164,9 +180,13 @@ slat_csr_view slat_csr_view_of(const slat_csr *m) {
 slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m) {
     if (!ctx || !m) return SLAT_EINVAL;
     (void)hipSetDevice(ctx->device);
-    if (m->row_ptr) (void)hipFreeAsync(m->row_ptr, ctx->stream);
-    if (m->col_idx) (void)hipFreeAsync(m->col_idx, ctx->stream);
-    if (m->values) (void)hipFreeAsync(m->values, ctx->stream);
+    if (m->alloc == kAllocJoint) {
+        if (m->row_ptr) (void)hipFreeAsync(m->row_ptr, ctx->stream);
+    } else {
+        if (m->row_ptr) (void)hipFreeAsync(m->row_ptr, ctx->stream);
+        if (m->col_idx) (void)hipFreeAsync(m->col_idx, ctx->stream);
+        if (m->values) (void)hipFreeAsync(m->values, ctx->stream);
+    }
     std::memset(m, 0, sizeof *m);
     return SLAT_OK;
 }
@@ -204,9 +224,7 @@ extern "C" slat_status slat_csr_create(slat_ctx *ctx, const slat_csr_view *src, 
     std::memset(out, 0, sizeof *out);
     const size_t vs = vsize(src->dtype);
     const hipMemcpyKind kind = src->residency == SLAT_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-    SLAT_HIP(ctx, hipMallocAsync((void **)&out->row_ptr, (src->n_rows + 1) * 8, ctx->stream));
-    SLAT_HIP(ctx, hipMallocAsync((void **)&out->col_idx, std::max<uint64_t>(src->nnz, 1) * 4, ctx->stream));
-    SLAT_HIP(ctx, hipMallocAsync(&out->values, std::max<uint64_t>(src->nnz, 1) * vs, ctx->stream));
+    SLAT_HIP(ctx, alloc_joint(out, src->n_rows, src->nnz, vs, ctx->stream));
     if (src->n_rows)
         SLAT_HIP(ctx, hipMemcpyAsync(out->row_ptr, src->row_ptr, (src->n_rows + 1) * 8, kind, ctx->stream));
     else
@@ -306,7 +324,7 @@ static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStre
 template <typename S>
 static hipError_t launch_build_ell(hipStream_t s, const slat_csr_view *B, uint32_t wq, uint32_t *ecol, void *eval,
                                    uint8_t *eng, unsigned long long *vmax, uint32_t epoch) {
-    const uint64_t blocks = std::min<uint64_t>((B->n_rows + kBlock - 1) / kBlock, 4096);
+    const uint64_t blocks = std::min<uint64_t>((B->n_rows * wq + kBlock - 1) / kBlock, 4096);
     hipLaunchKernelGGL(k_build_ell<S>, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(kBlock), 0, s, B->row_ptr,
                        B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng, vmax, epoch);
     return hipGetLastError();
@@ -351,6 +369,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if ((st = check_view(ctx, A, "A")) || (st = check_view(ctx, B, "B"))) return st;
     if (A->dtype != B->dtype) return fail(ctx, SLAT_EINVAL, "A and B value types differ");
     if (A->n_cols != B->n_rows) return fail(ctx, SLAT_EDIM, "A.n_cols != B.n_rows");
+    if (B->n_cols > 0xFFFFFFFFull - (1ull << 17))  // column ids are u32; the top 2^17 values stay free
+        return fail(ctx, SLAT_ENOTSUP, "n_cols too large for u32 column ids");
     if (row_begin > row_end || row_end > A->n_rows) return fail(ctx, SLAT_EINVAL, "bad row block");
     if (A->residency != SLAT_DEVICE || B->residency != SLAT_DEVICE) {
         // host inputs: stage through owned device copies (PCIe outside the engine's hot path)
@@ -387,12 +407,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     C->n_cols = ncols;
     C->dtype = dt;
     C->device = ctx->device;
-    SLAT_HIP(ctx, hipMallocAsync((void **)&C->row_ptr, (n + 1) * 8, s));
     if (n == 0 || ncols == 0 || A->nnz == 0 || B->nnz == 0) {
         // empty product: all-zero row_ptr
+        SLAT_HIP(ctx, alloc_joint(C, n, 0, vs, s));
         SLAT_HIP(ctx, hipMemsetAsync(C->row_ptr, 0, (n + 1) * 8, s));
-        SLAT_HIP(ctx, hipMallocAsync((void **)&C->col_idx, 4, s));
-        SLAT_HIP(ctx, hipMallocAsync(&C->values, 8, s));
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         return SLAT_OK;
     }
@@ -451,7 +469,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.shards = (unsigned long long *)(ws + o_sh);
     void *scan_tmp = ws + o_scan;
     size_t scan_tb = scan_b;
-    a.c_rp = C->row_ptr;
 
     // capacity by exact bound (no mid-call sync) unless it exceeds the budget
     unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
@@ -463,9 +480,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
     if (!exact) {
         C->capacity = (uint64_t)std::max<unsigned __int128>(bound128, 1);
-        SLAT_HIP(ctx, hipMallocAsync((void **)&C->col_idx, C->capacity * 4, s));
-        SLAT_HIP(ctx, hipMallocAsync(&C->values, C->capacity * vs, s));
+        SLAT_HIP(ctx, alloc_joint(C, n, C->capacity, vs, s));
+    } else {
+        SLAT_HIP(ctx, hipMallocAsync((void **)&C->row_ptr, (n + 1) * 8, s));
+        C->alloc = kAllocSeparate;
     }
+    a.c_rp = C->row_ptr;
 
     // LDS sizing and grid
     const int wpb = kBlock / kWave;
@@ -529,6 +549,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.c_col = C->col_idx;
     a.c_val = C->values;
     hipError_t e;
+    auto launch_num = [&](const Args &x) -> hipError_t {
+        if (dt == SLAT_U32) return launch_numeric<SemU32>(idx32, ell, grid, num_lds, s, x);
+        if (dt == SLAT_SAT64) return launch_numeric<SemSat64>(idx32, ell, grid, num_lds, s, x);
+        return launch_numeric<SemF64>(idx32, ell, grid, num_lds, s, x);
+    };
     if (ablate & ~7u) {
         // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
         // the real numeric pass below overwrites everything it wrote
@@ -536,44 +561,22 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         abl.ablate = ablate;
         abl.counts = (uint64_t *)(ws + o_abl);
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
-        if (dt == SLAT_U32)
-            e = launch_numeric<SemU32>(idx32, ell, grid, num_lds, s, abl);
-        else if (dt == SLAT_SAT64)
-            e = launch_numeric<SemSat64>(idx32, ell, grid, num_lds, s, abl);
-        else
-            e = launch_numeric<SemF64>(idx32, ell, grid, num_lds, s, abl);
-        SLAT_HIP(ctx, e);
+        SLAT_HIP(ctx, launch_num(abl));
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
     }
-    if (dt == SLAT_U32)
-        e = launch_numeric<SemU32>(idx32, ell, grid, num_lds, s, a);
-    else if (dt == SLAT_SAT64)
-        e = launch_numeric<SemSat64>(idx32, ell, grid, num_lds, s, a);
-    else
-        e = launch_numeric<SemF64>(idx32, ell, grid, num_lds, s, a);
-    SLAT_HIP(ctx, e);
+    SLAT_HIP(ctx, launch_num(a));
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
     SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                  hipMemcpyDeviceToHost, s));
     SLAT_HIP(ctx, hipStreamSynchronize(s));
-
-    if (SLAT_PHASES) {
-        // diagnostic build: per-phase cycles of the numeric kernel, summed over waves
-        unsigned long long ph[kPhaseSlots * 64];
-        SLAT_HIP(ctx, hipMemcpy(ph, a.shards + 512, sizeof ph, hipMemcpyDeviceToHost));
-        double tot[kPhaseSlots] = {};
-        for (int sh = 0; sh < 64; ++sh)
-            for (int i = 0; i < kPhaseSlots; ++i) tot[i] += (double)ph[sh * kPhaseSlots + i];
-        std::fprintf(stderr, "phases(rows=%.0f):", tot[kPhaseSlots - 1]);
-        for (int i = 0; i < kPhaseSlots - 1; ++i) std::fprintf(stderr, " %d:%.0f", i, tot[i] / std::max(1.0, tot[kPhaseSlots - 1]));
-        std::fprintf(stderr, "\n");
-    }
-    uint64_t nnz = ctx->h_shards[0], maxrow = 0, drops = 0, flops = 0;
+    uint64_t maxrow = 0, drops = 0, flops = 0;
     for (int i = 0; i < kShards; ++i) {
         maxrow = std::max<uint64_t>(maxrow, ctx->h_shards[i * kShardStride + 1]);
         drops += ctx->h_shards[i * kShardStride + 2];
         flops += ctx->h_shards[i * kShardStride + 3];
     }
+    const uint64_t nnz0 = ctx->h_shards[0];
+    uint64_t nnz = nnz0;
     double compact_ms = 0;
     if (drops) {
         // exact zeros were dropped: rebuild row_ptr from the per-row actual counts and move rows
@@ -597,13 +600,13 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             e = launch_compact<SemF64>(sym_grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
         SLAT_HIP(ctx, e);
         if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
-        (void)hipFreeAsync(C->row_ptr, s);
-        (void)hipFreeAsync(C->col_idx, s);
-        (void)hipFreeAsync(C->values, s);
+        slat_csr old = *C;
+        (void)slat_csr_free(ctx, &old);
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         C->row_ptr = nrp;
         C->col_idx = ncol;
         C->values = nval;
+        C->alloc = kAllocSeparate;
         C->capacity = std::max<uint64_t>(total, 1);
         nnz = total;
         if (timing) {

@@ -256,17 +256,27 @@ template <typename S>
 __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const uint32_t *col, const S *val,
                                                        uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng,
                                                        unsigned long long *vmax, uint32_t epoch) {
+    // one thread per (row k, group t): 4 columns and 4 values, written as whole groups
     uint32_t mx = 0;
-    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t total = (uint64_t)n * wq;
+    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = g / wq;
+        const uint32_t t = (uint32_t)(g - k * wq);
         const uint64_t s0 = rp[k], len = rp[k + 1] - s0;
-        eng[k] = (uint8_t)((len + 3) / 4);
-        for (uint32_t u = 0; u < wq * 4; ++u) {
-            const uint64_t o = k * wq * 4 + u;
-            ecol[o] = u < len ? col[s0 + u] : kSent;
-            eval[o] = u < len ? val[s0 + u] : S(0);
+        if (t == 0) eng[k] = (uint8_t)((len + 3) / 4);
+        uint32_t c[4];
+        S v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint64_t u = (uint64_t)t * 4 + e;
+            c[e] = u < len ? col[s0 + u] : kSent;
+            v[e] = u < len ? val[s0 + u] : S(0);
             if constexpr (std::is_same<S, uint32_t>::value)
-                if (u < len) mx = max(mx, (uint32_t)val[s0 + u]);
+                if (u < len) mx = max(mx, (uint32_t)v[e]);
         }
+        ((uint4 *)ecol)[g] = make_uint4(c[0], c[1], c[2], c[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) eval[g * 4 + e] = v[e];
     }
     if constexpr (std::is_same<S, uint32_t>::value) {
         // max B value, one atomic per block; the epoch in the high word supersedes earlier calls'
@@ -332,6 +342,13 @@ __device__ __forceinline__ Quad<typename Sem::S> prods(typename Sem::S a, const 
     return pr;
 }
 
+// u32 products of a row whose bound max(A) * max(B) * len < 2^32 holds: no clamp needed
+struct SemU32Narrow {
+    using S = uint32_t;
+    static constexpr bool kNarrowable = true;
+    __device__ static __forceinline__ S prod(S a, S b) { return a * b; }
+};
+
 // passes that need no values (symbolic, bitmap, column span) walk with this stand-in semiring
 struct SemNone {
     using S = uint32_t;
@@ -383,10 +400,11 @@ __device__ __forceinline__ void walk_row(const Args &p, I a0, I a1, G &&grp) {
     }
 }
 
-// window offset of column c: valid iff c is a real column inside [wlo, wlo + WIN)
+// window offset of column c: valid iff c is a real column inside [wlo, wlo + WIN). The padding
+// sentinel never lands in a window: the host rejects n_cols > 2^32 - 2^17 (WIN < 2^16).
 __device__ __forceinline__ bool win_off(uint32_t c, uint32_t wlo, uint32_t WIN, uint32_t &off) {
     off = c - wlo;
-    return c != kSent && off < WIN;
+    return off < WIN;  // kSent - wlo >= WIN because the host keeps n_cols <= 2^32 - 2^17
 }
 
 
@@ -418,8 +436,10 @@ __device__ __forceinline__ uint2 rank_word(const uint2 *W, uint32_t c, uint32_t 
     return W[ok ? (off >> 5) : 0u];
 }
 __device__ __forceinline__ uint32_t rank_in(uint2 w, uint32_t off, bool ok, uint32_t r0, uint32_t nch) {
-    const uint32_t r = w.y + __popc(w.x & ((1u << (off & 31)) - 1u)) - r0;
-    return (ok & (r < nch)) ? r : kSent;
+    // popc of the word's bits below the column (bitfield extract) plus the word's base rank
+    const uint32_t r = __builtin_amdgcn_ubfe(w.x, 0u, off & 31u);
+    const uint32_t rk = __builtin_popcount(r) + (w.y - r0);
+    return (ok & (rk < nch)) ? rk : kSent;
 }
 
 constexpr int kRegQ = 4;  // A entries per lane kept in registers across the numeric passes
@@ -617,8 +637,8 @@ struct RowWalker {
         if (nb > kNB) nb = kOvf;
     }
 
-    // grp(c4, pr4) / grp.multi(c4[kRegQ], pr4[kRegQ]) for every group; products when VV
-    template <bool VV, typename G>
+    // grp(c4, pr4) / grp.multi(c4[kRegQ], pr4[kRegQ]) for every group; products (PSem) when VV
+    template <bool VV, typename PSem = Sem, typename G>
     __device__ __forceinline__ void each_group(G &grp) {
         if constexpr (ELL) {
             for (uint32_t sg = 0; sg < nseg; ++sg) {
@@ -649,9 +669,9 @@ struct RowWalker {
                     if constexpr (VV) pt1 = ell_vals<S>(p, bk1, bt1);
                 }
                 if constexpr (VV) {
-                    sfor<kRegQ>([&](auto Q) { pq[Q] = prods<Sem>(aq[Q], pq[Q]); });
-                    pt0 = prods<Sem>(ba0, pt0);
-                    pt1 = prods<Sem>(ba1, pt1);
+                    sfor<kRegQ>([&](auto Q) { pq[Q] = prods<PSem>(aq[Q], pq[Q]); });
+                    pt0 = prods<PSem>(ba0, pt0);
+                    pt1 = prods<PSem>(ba1, pt1);
                 }
                 grp.multi(cq, pq);
                 if (nb > 0) grp(ct0, pt0);
@@ -974,7 +994,10 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                                 });
                         } else if (!(p.ablate & 8u)) {
                             AccPass<Sem, NW> acc{W, vals, cols, wlo, WIN, r0, nch, &pc, p.ablate};
-                            each_group(acc, std::true_type{});
+                            if constexpr (NW)
+                                rw.template each_group<true, SemU32Narrow>(acc);
+                            else
+                                rw.template each_group<true>(acc);
                         }
                         wave_sync();
                         if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);

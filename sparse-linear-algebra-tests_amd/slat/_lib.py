@@ -40,7 +40,8 @@ class CsrView(C.Structure):
 class CsrOwned(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_uint64), ("nnz", C.c_uint64), ("capacity", C.c_uint64),
                 ("max_row_nnz", C.c_uint64), ("row_ptr", C.c_void_p), ("col_idx", C.c_void_p),
-                ("values", C.c_void_p), ("dtype", C.c_int32), ("device", C.c_int32)]
+                ("values", C.c_void_p), ("dtype", C.c_int32), ("device", C.c_int32), ("alloc", C.c_int32),
+                ("_pad", C.c_int32)]
 
 
 class Stats(C.Structure):
