@@ -84,8 +84,8 @@ def load_pmc(workload: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50, help="untimed steps; the GPU needs ~10 ms of load to clock up")
     ap.add_argument("--side", type=int, default=30)
     ap.add_argument("--power", type=int, default=7, help="C = A^(power-1) * A")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")

@@ -97,6 +97,11 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SLAT_ENODEV;
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SLAT_ENODEV;
+    if (const char *e_ = std::getenv("SLAT_SPIN"))  // experiment: spin-wait stream syncs
+        if (std::atoi(e_)) {
+            (void)hipSetDevice(device);
+            (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+        }
     slat_ctx *ctx = new slat_ctx();
     ctx->device = device;
     ctx->cu_count = prop.multiProcessorCount;
@@ -123,7 +128,7 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         delete ctx;
         return SLAT_EOOM;
     }
-    for (auto &e : ctx->ev) (void)hipEventCreate(&e);
+    for (auto &e : ctx->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);  // timing only
     *out = ctx;
     return SLAT_OK;
 }
@@ -310,6 +315,23 @@ static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hi
     return hipGetLastError();
 }
 
+// resident blocks per CU of the numeric kernel instance (its grid is sized to that: the product
+// record in the workspace is indexed by resident wave)
+template <typename Sem>
+static int numeric_blocks_per_cu(bool idx32, bool ell, size_t lds) {
+    int nb = 0;
+    hipError_t e;
+    if (idx32 && ell)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint32_t, true>, kBlock, lds);
+    else if (idx32)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint32_t, false>, kBlock, lds);
+    else if (ell)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint64_t, true>, kBlock, lds);
+    else
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint64_t, false>, kBlock, lds);
+    return (e == hipSuccess && nb > 0) ? nb : 1;
+}
+
 static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
     if (idx32 && ell)
         hipLaunchKernelGGL((k_symbolic<uint32_t, true>), grid, dim3(kBlock), lds, s, a);
@@ -444,6 +466,22 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows * wq * 4 < (1ull << 32) && !std::getenv("SLAT_NO_ELL");
 
+    // LDS sizing and grids. The numeric grid is the kernel's resident capacity (waves stride over
+    // rows; measured faster than oversubscribing); symbolic takes up to 16 blocks per CU.
+    const int wpb = kBlock / kWave;
+    if (const char *e_ = std::getenv("SLAT_CAP")) a.area = 6 * std::max(64, std::atoi(e_));  // tuning knob
+    a.area = (a.area + 15) & ~15u;
+    const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.area).bytes;
+    if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
+    const size_t sym_lds = (size_t)wpb * asym.ww * 4;
+    const uint64_t row_blocks = (n + wpb - 1) / wpb;
+    const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * 16)));
+    const int nbpc = dt == SLAT_U32     ? numeric_blocks_per_cu<SemU32>(idx32, ell, num_lds)
+                     : dt == SLAT_SAT64 ? numeric_blocks_per_cu<SemSat64>(idx32, ell, num_lds)
+                                        : numeric_blocks_per_cu<SemF64>(idx32, ell, num_lds);
+    const dim3 grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc)));
+    const bool timing = flags & SLAT_FLAG_TIMING;
+
     // workspace: counts [n] | ablation counts [n] | shards | scan temp | ELL cols | ELL vals | ELL groups
     auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t counts_b = up256(n * 8);
@@ -487,17 +525,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     a.c_rp = C->row_ptr;
 
-    // LDS sizing and grid
-    const int wpb = kBlock / kWave;
-    if (const char *e_ = std::getenv("SLAT_CAP")) a.area = 6 * std::max(64, std::atoi(e_));  // tuning knob
-    a.area = (a.area + 15) & ~15u;
-    const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.area).bytes;
-    if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
-    const size_t sym_lds = (size_t)wpb * asym.ww * 4;
-    const uint64_t max_blocks = (uint64_t)ctx->cu_count * 16;
-    const dim3 grid((unsigned)std::max<uint64_t>(1, std::min((n + wpb - 1) / wpb, max_blocks)));
-    const dim3 sym_grid = grid;
-    const bool timing = flags & SLAT_FLAG_TIMING;
 
     if (a.stats || SLAT_PHASES) SLAT_HIP(ctx, hipMemsetAsync(a.shards, 0, shards_b, s));
     asym.counts = a.counts;

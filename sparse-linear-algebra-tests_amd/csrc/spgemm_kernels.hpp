@@ -342,13 +342,6 @@ __device__ __forceinline__ Quad<typename Sem::S> prods(typename Sem::S a, const 
     return pr;
 }
 
-// u32 products of a row whose bound max(A) * max(B) * len < 2^32 holds: no clamp needed
-struct SemU32Narrow {
-    using S = uint32_t;
-    static constexpr bool kNarrowable = true;
-    __device__ static __forceinline__ S prod(S a, S b) { return a * b; }
-};
-
 // passes that need no values (symbolic, bitmap, column span) walk with this stand-in semiring
 struct SemNone {
     using S = uint32_t;
@@ -994,10 +987,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                                 });
                         } else if (!(p.ablate & 8u)) {
                             AccPass<Sem, NW> acc{W, vals, cols, wlo, WIN, r0, nch, &pc, p.ablate};
-                            if constexpr (NW)
-                                rw.template each_group<true, SemU32Narrow>(acc);
-                            else
-                                rw.template each_group<true>(acc);
+                            each_group(acc, std::true_type{});
                         }
                         wave_sync();
                         if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
