@@ -596,6 +596,18 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                  hipMemcpyDeviceToHost, s));
     SLAT_HIP(ctx, hipStreamSynchronize(s));
+    if (SLAT_PHASES) {
+        // diagnostic build: per-phase cycles of the numeric kernel, summed over waves
+        unsigned long long ph[kPhaseSlots * 64];
+        SLAT_HIP(ctx, hipMemcpy(ph, a.shards + 512, sizeof ph, hipMemcpyDeviceToHost));
+        double tot[kPhaseSlots] = {};
+        for (int sh = 0; sh < 64; ++sh)
+            for (int i = 0; i < kPhaseSlots; ++i) tot[i] += (double)ph[sh * kPhaseSlots + i];
+        std::fprintf(stderr, "phases(rows=%.0f):", tot[kPhaseSlots - 1]);
+        for (int i = 0; i < kPhaseSlots - 1; ++i)
+            std::fprintf(stderr, " %d:%.0f", i, tot[i] / std::max(1.0, tot[kPhaseSlots - 1]));
+        std::fprintf(stderr, "\n");
+    }
     uint64_t maxrow = 0, drops = 0, flops = 0;
     for (int i = 0; i < kShards; ++i) {
         maxrow = std::max<uint64_t>(maxrow, ctx->h_shards[i * kShardStride + 1]);

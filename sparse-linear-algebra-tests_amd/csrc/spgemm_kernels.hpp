@@ -342,6 +342,13 @@ __device__ __forceinline__ Quad<typename Sem::S> prods(typename Sem::S a, const 
     return pr;
 }
 
+// u32 products of a row whose bound max(A) * max(B) * len < 2^32 holds: no clamp needed
+struct SemU32Narrow {
+    using S = uint32_t;
+    static constexpr bool kNarrowable = true;
+    __device__ static __forceinline__ S prod(S a, S b) { return a * b; }
+};
+
 // passes that need no values (symbolic, bitmap, column span) walk with this stand-in semiring
 struct SemNone {
     using S = uint32_t;
@@ -409,30 +416,30 @@ struct NumLayout {
     uint32_t off_slots, bytes;
 };
 
-// Per-wave LDS region: W ww*8 (uint2 per bitmap word: .x column bits, .y rank of the word's first
-// column, so a rank lookup is ONE ds_read_b64) | rank slots `area` bytes: values, then u16 column
-// offsets within the window
+// Per-wave LDS region: W (ww+1)*8 (uint2 per bitmap word: .x column bits, .y rank of the word's
+// first column, so a rank lookup is ONE ds_read_b64; W[ww] = {0, 2^31} catches every column outside
+// the window, whose rank then fails the chunk test) | rank slots `area` bytes: values, then u16
+// column offsets within the window
 __host__ __device__ inline NumLayout num_layout(uint32_t ww, uint32_t area) {
     auto up = [](uint32_t x, uint32_t a) { return (x + a - 1) / a * a; };
     NumLayout L;
-    L.off_slots = up(ww * 8, 16);
+    L.off_slots = up((ww + 1) * 8, 16);  // + W[ww]: the dummy word of out-of-window columns
     L.bytes = up(L.off_slots + area, 16);
     return L;
 }
 
-// rank (within chunk [r0, r0 + nch)) of column c, or kSent. The LDS read happens for every lane
-// (word 0 for columns outside the window) and the predicate is a non-short-circuit AND on the
-// loaded value, so a batch issues all its lookups before it waits on any.
-__device__ __forceinline__ uint2 rank_word(const uint2 *W, uint32_t c, uint32_t wlo, uint32_t WIN, uint32_t &off,
-                                           bool &ok) {
-    ok = win_off(c, wlo, WIN, off);
-    return W[ok ? (off >> 5) : 0u];
+// rank (within chunk [r0, r0 + nch)) of column c, or kSent. The word index is clamped to the dummy
+// word W[ww] (no bits, base 2^31) instead of tested: out-of-window and padding columns read it and
+// fail the chunk test. The LDS read happens for every lane, so a batch issues all its lookups
+// before it waits on any.
+__device__ __forceinline__ uint2 rank_word(const uint2 *W, uint32_t ww, uint32_t c, uint32_t wlo, uint32_t &off) {
+    off = c - wlo;
+    return W[min(off >> 5, ww)];
 }
-__device__ __forceinline__ uint32_t rank_in(uint2 w, uint32_t off, bool ok, uint32_t r0, uint32_t nch) {
-    // popc of the word's bits below the column (bitfield extract) plus the word's base rank
-    const uint32_t r = __builtin_amdgcn_ubfe(w.x, 0u, off & 31u);
-    const uint32_t rk = __builtin_popcount(r) + (w.y - r0);
-    return (ok & (rk < nch)) ? rk : kSent;
+__device__ __forceinline__ uint32_t rank_in(uint2 w, uint32_t off, uint32_t r0, uint32_t nch) {
+    // popc of the word's bits below the column (v_bfe masks the width to 5 bits) plus the word's rank
+    const uint32_t rk = __builtin_popcount(__builtin_amdgcn_ubfe(w.x, 0u, off)) + (w.y - r0);
+    return rk < nch ? rk : kSent;
 }
 
 constexpr int kRegQ = 4;  // A entries per lane kept in registers across the numeric passes
@@ -725,14 +732,12 @@ struct AccPass {
     const uint2 *W;
     void *vals;
     uint16_t *cols;  // column offset within the window
-    uint32_t wlo, WIN, r0, nch;
+    uint32_t ww, wlo, r0, nch;
     PhaseClock *pc;
-    uint32_t abl;  // experiments: 64 no column stores, 128 no value atomics, 256 hashed ranks (no reads)
     template <int Q>
     __device__ __forceinline__ void run(const uint4 *c, const Quad<S> *pr_in) {
         uint2 w[Q][4];
         uint32_t off[Q][4];
-        bool ok[Q][4];
         S pr[Q][4];
         // products pinned in VGPRs up front: keeps B-value loads out of the per-slot branches
 #pragma unroll
@@ -746,14 +751,7 @@ struct AccPass {
         for (int q = 0; q < Q; ++q) {
             const uint32_t cc[4] = {c[q].x, c[q].y, c[q].z, c[q].w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (abl & 256u) {
-                    ok[q][e] = win_off(cc[e], wlo, WIN, off[q][e]);
-                    w[q][e] = make_uint2(0xFFFFFFFFu, (cc[e] * 2654435761u) >> 23);
-                } else {
-                    w[q][e] = rank_word(W, cc[e], wlo, WIN, off[q][e], ok[q][e]);
-                }
-            }
+            for (int e = 0; e < 4; ++e) w[q][e] = rank_word(W, ww, cc[e], wlo, off[q][e]);
         }
         if constexpr (SLAT_PHASES) {
             pin(w[0][0].x);
@@ -763,24 +761,20 @@ struct AccPass {
         for (int q = 0; q < Q; ++q) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const uint32_t r = rank_in(w[q][e], off[q][e], ok[q][e], r0, nch);
+                const uint32_t r = rank_in(w[q][e], off[q][e], r0, nch);
                 if (r != kSent) {
-                    if (!(abl & 128u)) {
-                        if constexpr (NARROW)
-                            atomicAdd((uint32_t *)vals + r, (uint32_t)pr[q][e]);
-                        else
-                            Sem::acc((typename Sem::V *)vals, r, pr[q][e]);
-                    }
-                    if (!(abl & 64u)) cols[r] = (uint16_t)off[q][e];
+                    if constexpr (NARROW)
+                        atomicAdd((uint32_t *)vals + r, (uint32_t)pr[q][e]);
+                    else
+                        Sem::acc((typename Sem::V *)vals, r, pr[q][e]);
+                    cols[r] = (uint16_t)off[q][e];
                 }
             }
         }
         if constexpr (SLAT_PHASES) pc->mark(11);  // atomics issued
     }
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) { run<1>(&c, &pr); }
-    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
-        sfor<kRegQ / 2>([&](auto H) { run<2>(c + 2 * H, pr + 2 * H); });
-    }
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) { run<kRegQ>(c, pr); }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -894,6 +888,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
 
     if (blockIdx.x == 0 && threadIdx.x == 0) p.shards[0] = p.c_rp[p.nrows];
     for (uint32_t w = lane; w < p.ww; w += kWave) W[w] = make_uint2(0u, 0u);
+    if (lane == 0) W[p.ww] = make_uint2(0u, 0x80000000u);  // dummy word: never set, never cleared
     wave_sync();
 
     const uint32_t WIN = p.ww * 32;
@@ -977,17 +972,19 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                             if (!(p.ablate & 8u))
                                 traverse_ordered<I, S>(p, a0, a1, [&](uint32_t j, S a, S b) {
                                     uint32_t off;
-                                    bool ok;
-                                    const uint2 w = rank_word(W, j, wlo, WIN, off, ok);
-                                    const uint32_t r = rank_in(w, off, ok, r0, nch);
+                                    const uint2 w = rank_word(W, p.ww, j, wlo, off);
+                                    const uint32_t r = rank_in(w, off, r0, nch);
                                     if (r != kSent) {
                                         Sem::acc((V *)vals, r, Sem::prod(a, b));
                                         cols[r] = (uint16_t)off;
                                     }
                                 });
                         } else if (!(p.ablate & 8u)) {
-                            AccPass<Sem, NW> acc{W, vals, cols, wlo, WIN, r0, nch, &pc, p.ablate};
-                            each_group(acc, std::true_type{});
+                            AccPass<Sem, NW> acc{W, vals, cols, p.ww, wlo, r0, nch, &pc};
+                            if constexpr (NW)
+                                rw.template each_group<true, SemU32Narrow>(acc);
+                            else
+                                rw.template each_group<true>(acc);
                         }
                         wave_sync();
                         if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
