@@ -464,7 +464,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const uint64_t wq = (maxrow_b + 3) / 4;
     const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
-                     B->n_rows * wq * 4 < (1ull << 32) && !std::getenv("SLAT_NO_ELL");
+                     B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
+                     !std::getenv("SLAT_NO_ELL");  // 24-bit row index, 31-bit byte offsets in the kernels
 
     // LDS sizing and grids. The numeric grid is the kernel's resident capacity (waves stride over
     // rows; measured faster than oversubscribing); symbolic takes up to 16 blocks per CU.

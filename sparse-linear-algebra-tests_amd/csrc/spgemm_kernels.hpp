@@ -297,19 +297,23 @@ struct Quad {
     S v[4];
 };
 
-// the t-th group of 4 values of ELL row k
+// the t-th group of 4 values / columns of ELL row k. The host keeps B's ELL image below 2^24 rows and
+// 2^31 bytes, so the byte offset is one 24-bit multiply-add and the load takes the SGPR-base +
+// 32-bit VGPR-offset form (no 64-bit address math per lane).
 template <typename S>
 __device__ __forceinline__ Quad<S> ell_vals(const Args &p, uint32_t k, uint32_t t) {
+    constexpr uint32_t kGB = 4 * sizeof(S);  // bytes per group of 4 values
+    const uint32_t off = __umul24(k, p.ell_wq * kGB) + t * kGB;
+    const uint8_t *b = (const uint8_t *)p.ell_val + off;
     Quad<S> q;
     if constexpr (sizeof(S) == 4) {
-        const uint4 x = ((const uint4 *)p.ell_val)[(size_t)k * p.ell_wq + t];
+        const uint4 x = *(const uint4 *)b;
         q.v[0] = __builtin_bit_cast(S, x.x);
         q.v[1] = __builtin_bit_cast(S, x.y);
         q.v[2] = __builtin_bit_cast(S, x.z);
         q.v[3] = __builtin_bit_cast(S, x.w);
     } else {
-        const uint4 *b = (const uint4 *)p.ell_val + ((size_t)k * p.ell_wq + t) * 2;
-        const uint4 x = b[0], y = b[1];
+        const uint4 x = ((const uint4 *)b)[0], y = ((const uint4 *)b)[1];
         q.v[0] = __builtin_bit_cast(S, ((uint64_t)x.y << 32) | x.x);
         q.v[1] = __builtin_bit_cast(S, ((uint64_t)x.w << 32) | x.z);
         q.v[2] = __builtin_bit_cast(S, ((uint64_t)y.y << 32) | y.x);
@@ -319,7 +323,8 @@ __device__ __forceinline__ Quad<S> ell_vals(const Args &p, uint32_t k, uint32_t 
 }
 
 __device__ __forceinline__ uint4 ell_cols(const Args &p, uint32_t k, uint32_t t) {
-    return ((const uint4 *)p.ell_col)[(size_t)k * p.ell_wq + t];
+    const uint32_t off = __umul24(k, p.ell_wq * 16u) + t * 16u;
+    return *(const uint4 *)((const uint8_t *)p.ell_col + off);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -581,14 +586,18 @@ struct RowWalker {
     __device__ __forceinline__ void load_seg(I sb) {
         const int lane = lane_id();
         const S *av_ = (const S *)p.a_val;
+        // wave-uniform segment base + a 32-bit lane offset (SGPR-base addressing, no 64-bit math)
+        const uint32_t *seg_c = p.a_col + sb;
+        const S *seg_v = av_ + sb;
+        const uint32_t seg_n = (uint32_t)min<uint64_t>((uint64_t)(a1 - sb), kSeg);
         sfor<kRegQ>([&](auto Q) {
             constexpr int q = Q;
-            const I idx = sb + (I)(q * kWave + lane);
+            const uint32_t j = (uint32_t)(q * kWave + lane);
             kq[q] = kSent;
             aq[q] = S(0);
-            if (idx < a1) {
-                kq[q] = p.a_col[idx];
-                if constexpr (AVALS) aq[q] = av_[idx];
+            if (j < seg_n) {
+                kq[q] = seg_c[j];
+                if constexpr (AVALS) aq[q] = seg_v[j];
             }
         });
         sfor<kRegQ>([&](auto Q) {
@@ -800,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     constexpr int kWpb = kBlock / kWave;
     const int lane = lane_id();
-    const int wv = threadIdx.x / kWave;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
     uint32_t *L0 = smem + (size_t)wv * p.ww;
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) p.c_rp[0] = 0;
@@ -870,7 +879,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     __shared__ uint32_t red[2][kWpb];
 
     const int lane = lane_id();
-    const int wv = threadIdx.x / kWave;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
     const NumLayout lay = num_layout(p.ww, p.area);
     uint8_t *region = smem8 + (size_t)wv * lay.bytes;
     uint2 *W = (uint2 *)region;
@@ -990,6 +999,10 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                         if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
                         mark(12);  // accumulate pass drain
                         // 4. emit at the row's slice, coalesced
+                        // wave-uniform output base + 32-bit lane offsets
+                        uint32_t *oc = p.c_col + out_pos;
+                        S *ov = cval + out_pos;
+                        const uint32_t lim = (uint32_t)min<uint64_t>(out_end - min(out_pos, out_end), nch);
                         for (uint32_t t = lane; t < nch; t += kWave) {
                             S v;
                             if constexpr (NW)
@@ -997,9 +1010,9 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                             else
                                 v = Sem::finish((const V *)vals, t);
                             zeros += Sem::is_zero(v) ? 1u : 0u;
-                            if (out_pos + t < out_end && !(p.ablate & 16u)) {  // never trust blindly
-                                p.c_col[out_pos + t] = wlo + cols[t];
-                                cval[out_pos + t] = v;
+                            if (t < lim && !(p.ablate & 16u)) {  // never write past the row's slice
+                                oc[t] = wlo + cols[t];
+                                ov[t] = v;
                             }
                         }
                         out_pos += nch;
