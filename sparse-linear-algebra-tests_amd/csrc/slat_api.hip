@@ -6,11 +6,10 @@
 //      so no host round trip is needed between the symbolic and numeric passes; the capacity is
 //      recorded in slat_csr.capacity. SLAT_FLAG_EXACT_ALLOC (or a bound above the memory budget)
 //      takes the reference's exact-size path instead: sync after the scan, allocate nnz(C).
-//   2. k_symbolic -> hipcub::DeviceScan::InclusiveSum -> k_numeric, all stream-ordered.
+//   2. k_symbolic -> k_scan_rows (single-pass look-back scan) -> k_numeric, all stream-ordered.
 //   3. One D2H of the 64 status shards (nnz, max row nnz, dropped-zero rows) + stream sync.
 //   4. Rare: k_compact when explicit zeros were dropped.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -33,9 +32,16 @@ struct slat_ctx {
     // workspace (grown on demand)
     void *ws = nullptr;
     size_t ws_bytes = 0;
-    unsigned long long *h_shards = nullptr;  // pinned, mapped
-    unsigned long long *d_vmax = nullptr;    // (epoch << 32) | max B value, written by k_build_ell
+    unsigned long long *h_shards = nullptr;  // pinned (stats / max-row read-backs)
+    unsigned long long *h_out = nullptr;     // mapped pinned: [0] nnz, [1] max row nnz, [2] rows with zeros
+    unsigned long long *h_out_dev = nullptr; // its device alias (written by k_scan_rows / k_numeric)
+    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word
+    unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
+    unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
+    uint64_t status_cap = 0;                 // tiles d_status holds
+    unsigned long long ticket_base = 0;      // tiles handed out so far (the ticket is monotonic)
+    uint32_t scan_epoch = 0;                 // tag of the status / max-row words (22 bits)
     hipEvent_t ev[6] = {};
     slat_stats stats = {};
 };
@@ -122,12 +128,15 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         delete ctx;
         return SLAT_EOOM;
     }
-    if (hipMalloc((void **)&ctx->d_vmax, 16) != hipSuccess || hipMemset(ctx->d_vmax, 0, 16) != hipSuccess) {
+    if (hipMalloc((void **)&ctx->d_words, 64) != hipSuccess || hipMemset(ctx->d_words, 0, 64) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_out, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&ctx->h_out_dev, ctx->h_out, 0) != hipSuccess) {
         (void)hipHostFree(ctx->h_shards);
         (void)hipStreamDestroy(ctx->own_stream);
         delete ctx;
         return SLAT_EOOM;
     }
+    ctx->d_vmax = ctx->d_words;
     for (auto &e : ctx->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);  // timing only
     *out = ctx;
     return SLAT_OK;
@@ -139,7 +148,9 @@ slat_status slat_ctx_destroy(slat_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->h_shards) (void)hipHostFree(ctx->h_shards);
-    if (ctx->d_vmax) (void)hipFree(ctx->d_vmax);
+    if (ctx->d_words) (void)hipFree(ctx->d_words);
+    if (ctx->d_status) (void)hipFree(ctx->d_status);
+    if (ctx->h_out) (void)hipHostFree(ctx->h_out);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -360,11 +371,29 @@ static hipError_t launch_compact(dim3 grid, hipStream_t s, const uint64_t *orp, 
     return hipGetLastError();
 }
 
-static size_t scan_temp_bytes(uint64_t n) {
-    size_t tb = 0;
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, tb, (const uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
-    return (tb + 255) & ~(size_t)255;
+// row_ptr[0..n] of a count vector: k_scan_rows (one kernel); the total and the max count land in
+// ctx->h_out[0], [1] once the stream reaches that point
+static slat_status launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s) {
+    const uint64_t tiles = std::max<uint64_t>((n + kScanTile - 1) / kScanTile, 1);
+    if (tiles > ctx->status_cap) {
+        if (ctx->d_status) SLAT_HIP(ctx, hipFreeAsync(ctx->d_status, s));
+        const uint64_t cap = std::max<uint64_t>(tiles, 1024);
+        SLAT_HIP(ctx, hipMallocAsync((void **)&ctx->d_status, cap * 8, s));
+        SLAT_HIP(ctx, hipMemsetAsync(ctx->d_status, 0, cap * 8, s));
+        ctx->status_cap = cap;
+    }
+    if (++ctx->scan_epoch >= (1u << 22)) {  // tag wrap: clear every tagged word once
+        SLAT_HIP(ctx, hipMemsetAsync(ctx->d_status, 0, ctx->status_cap * 8, s));
+        SLAT_HIP(ctx, hipMemsetAsync(ctx->d_words + 2, 0, 8, s));
+        ctx->scan_epoch = 1;
+    }
+    hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status,
+                       ctx->d_words + 1, ctx->ticket_base, ctx->scan_epoch, ctx->d_words + 2, ctx->h_out_dev);
+    SLAT_HIP(ctx, hipGetLastError());
+    ctx->ticket_base += tiles;
+    return SLAT_OK;
 }
+
 
 // Window geometry for a group of `threads` lanes: ww = threads * per with `per` odd (thread-
 // contiguous word ownership is then free of LDS bank conflicts) and ww <= max_ww (u16 ranks need
@@ -487,10 +516,9 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t counts_b = up256(n * 8);
     const size_t shards_b = 4096 + (SLAT_PHASES ? 8192 : 0);  // + phase-timing slots (diagnostic builds)
-    const size_t scan_b = scan_temp_bytes(n);
     const size_t ecol_b = ell ? up256(B->n_rows * wq * 16) : 0, eval_b = ell ? up256(B->n_rows * wq * 4 * vs) : 0;
     const size_t eng_b = ell ? up256(B->n_rows) : 0;
-    const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_scan = o_sh + shards_b, o_ecol = o_scan + scan_b,
+    const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b;
     if ((st = ensure_ws(ctx, o_eng + eng_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
@@ -506,8 +534,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     a.counts = (uint64_t *)ws;
     a.shards = (unsigned long long *)(ws + o_sh);
-    void *scan_tmp = ws + o_scan;
-    size_t scan_tb = scan_b;
+    a.host_out = ctx->h_out_dev;
+    ctx->h_out[0] = ctx->h_out[1] = ctx->h_out[2] = 0;  // no kernel of this context is in flight
 
     // capacity by exact bound (no mid-call sync) unless it exceeds the budget
     unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
@@ -559,13 +587,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     launch_symbolic(idx32, ell, sym_grid, sym_lds, s, asym);
     SLAT_HIP(ctx, hipGetLastError());
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
-    SLAT_HIP(ctx, hipcub::DeviceScan::InclusiveSum(scan_tmp, scan_tb, a.counts, C->row_ptr + 1, (int)n, s));
+    if ((st = launch_scan(ctx, a.counts, n, C->row_ptr, s))) return st;
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
 
     if (exact) {
-        uint64_t total = 0;
-        SLAT_HIP(ctx, hipMemcpyAsync(&total, C->row_ptr + n, 8, hipMemcpyDeviceToHost, s));
         SLAT_HIP(ctx, hipStreamSynchronize(s));
+        const uint64_t total = ctx->h_out[0];
         C->capacity = std::max<uint64_t>(total, 1);
         if (hipMallocAsync((void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
             hipMallocAsync(&C->values, C->capacity * vs, s) != hipSuccess) {
@@ -594,8 +621,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     SLAT_HIP(ctx, launch_num(a));
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
-    SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
-                                 hipMemcpyDeviceToHost, s));
+    if (a.stats) SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
+                                             hipMemcpyDeviceToHost, s));
     SLAT_HIP(ctx, hipStreamSynchronize(s));
     if (SLAT_PHASES) {
         // diagnostic build: per-phase cycles of the numeric kernel, summed over waves
@@ -609,24 +636,21 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             std::fprintf(stderr, " %d:%.0f", i, tot[i] / std::max(1.0, tot[kPhaseSlots - 1]));
         std::fprintf(stderr, "\n");
     }
-    uint64_t maxrow = 0, drops = 0, flops = 0;
-    for (int i = 0; i < kShards; ++i) {
-        maxrow = std::max<uint64_t>(maxrow, ctx->h_shards[i * kShardStride + 1]);
-        drops += ctx->h_shards[i * kShardStride + 2];
-        flops += ctx->h_shards[i * kShardStride + 3];
-    }
-    const uint64_t nnz0 = ctx->h_shards[0];
+    // totals from the mapped host words (k_scan_rows: nnz, max row; k_numeric: rows with zeros)
+    uint64_t maxrow = ctx->h_out[1], drops = ctx->h_out[2], flops = 0;
+    if (a.stats)
+        for (int i = 0; i < kShards; ++i) flops += ctx->h_shards[i * kShardStride + 3];
+    const uint64_t nnz0 = ctx->h_out[0];
     uint64_t nnz = nnz0;
     double compact_ms = 0;
     if (drops) {
         // exact zeros were dropped: rebuild row_ptr from the per-row actual counts and move rows
         uint64_t *nrp = nullptr;
         SLAT_HIP(ctx, hipMallocAsync((void **)&nrp, (n + 1) * 8, s));
-        SLAT_HIP(ctx, hipMemsetAsync(nrp, 0, 8, s));
-        SLAT_HIP(ctx, hipcub::DeviceScan::InclusiveSum(scan_tmp, scan_tb, a.counts, nrp + 1, (int)n, s));
-        uint64_t total = 0;
-        SLAT_HIP(ctx, hipMemcpyAsync(&total, nrp + n, 8, hipMemcpyDeviceToHost, s));
+        if ((st = launch_scan(ctx, a.counts, n, nrp, s))) return st;
         SLAT_HIP(ctx, hipStreamSynchronize(s));
+        const uint64_t total = ctx->h_out[0];
+        maxrow = ctx->h_out[1];
         uint32_t *ncol = nullptr;
         void *nval = nullptr;
         SLAT_HIP(ctx, hipMallocAsync((void **)&ncol, std::max<uint64_t>(total, 1) * 4, s));

@@ -83,6 +83,7 @@ struct Args {
     const uint8_t *ell_ng;    // [n_B] groups of 4 holding real entries: ceil(len / 4)
     unsigned long long *b_vmax;  // (epoch << 32) | max B value, from k_build_ell (u32 only; else null)
     uint32_t epoch;
+    unsigned long long *host_out;  // mapped pinned host words: [0] nnz, [1] max row nnz, [2] rows with zeros
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
     uint32_t *c_col;
@@ -696,6 +697,8 @@ struct RowWalker {
     }
 };
 
+__device__ __forceinline__ void pin_u64(unsigned long long v) { pin(v); }
+
 // numeric pass 1: column span of the row (rows wider than one window)
 template <typename S>
 struct SpanPass {
@@ -876,7 +879,6 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     constexpr int kWpb = kBlock / kWave;
     constexpr bool kVals = !Sem::kOrdered;  // f64 accumulates from an ordered CSR walk
     extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
-    __shared__ uint32_t red[2][kWpb];
 
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
@@ -895,7 +897,6 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
         }
     S *cval = (S *)p.c_val;
 
-    if (blockIdx.x == 0 && threadIdx.x == 0) p.shards[0] = p.c_rp[p.nrows];
     for (uint32_t w = lane; w < p.ww; w += kWave) W[w] = make_uint2(0u, 0u);
     if (lane == 0) W[p.ww] = make_uint2(0u, 0x80000000u);  // dummy word: never set, never cleared
     wave_sync();
@@ -903,7 +904,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     const uint32_t WIN = p.ww * 32;
     const uint32_t per = p.ww / kWave;  // odd: lane-contiguous word ownership is conflict-free
     const uint32_t wb0 = lane * per;
-    uint32_t maxrow = 0, zrows = 0;
+    uint32_t zrows = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     PhaseClock pc{};
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
@@ -1036,7 +1037,6 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
         const uint32_t rz = p.ablate ? 0u : wave_sum_u32(zeros);  // ablation runs: no compaction
         const uint64_t got = out_pos - out_begin - rz;
         if (lane == 0) p.counts[row] = got;
-        maxrow = max(maxrow, (uint32_t)min<uint64_t>(got, 0xFFFFFFFFull));
         zrows += rz ? 1u : 0u;
     }
     mark(6);  // row tail (counts)
@@ -1046,21 +1046,105 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
             for (int i = 0; i < kPhaseSlots; ++i) atomicAdd(&dst[i], (unsigned long long)ph[i]);
         }
     }
-    if (lane == 0) {
-        red[0][wv] = maxrow;
-        red[1][wv] = zrows;
+    // rows that lost explicit zeros (rare): counted straight into the mapped host word
+    if (lane == 0 && zrows)
+        __hip_atomic_fetch_add(&p.host_out[2], (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ------------------------------------------------------------------------------------------------
+// row_ptr = inclusive scan of the row counts: ONE single-pass kernel (decoupled look-back). Tiles of
+// 8192 rows are taken in ticket order (a monotonic counter, so no reset), each publishes its
+// aggregate then its inclusive prefix in an epoch-tagged status word (no init kernel). The last
+// tile writes the total nnz and the max row nnz into mapped host memory (no copy in the stream).
+// ------------------------------------------------------------------------------------------------
+constexpr int kScanThreads = 1024, kScanItems = 8;
+constexpr uint64_t kScanTile = (uint64_t)kScanThreads * kScanItems;
+constexpr unsigned long long kStAgg = 1ull << 40, kStInc = 2ull << 40, kStVal = (1ull << 40) - 1;
+
+__device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long long v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const unsigned long long t = __shfl_up(v, d);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_t *counts, uint64_t n, uint64_t *rp,
+                                                            unsigned long long *status, unsigned long long *ticket,
+                                                            unsigned long long ticket_base, uint32_t epoch,
+                                                            unsigned long long *maxw, unsigned long long *host_out) {
+    __shared__ unsigned long long wsum[kScanThreads / kWave];
+    __shared__ unsigned long long s_bcast[2];
+    __shared__ uint32_t wmax[kScanThreads / kWave];
+    const int t = threadIdx.x, lane = lane_id(), w = t / kWave;
+    const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    const unsigned long long tag = (unsigned long long)epoch << 42;
+    auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto st = [](unsigned long long *x, unsigned long long v) {
+        __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (t == 0) s_bcast[0] = atomicAdd(ticket, 1ull) - ticket_base;
+    __syncthreads();
+    const uint64_t tile = s_bcast[0];
+    const uint64_t i0 = tile * kScanTile + (uint64_t)t * kScanItems;
+    unsigned long long v[kScanItems], run = 0;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int e = 0; e < kScanItems; ++e) v[e] = i0 + e < n ? counts[i0 + e] : 0ull;
+#pragma unroll
+    for (int e = 0; e < kScanItems; ++e) {
+        mx = max(mx, (uint32_t)min<unsigned long long>(v[e], 0xFFFFFFFFull));
+        run += v[e];
+        v[e] = run;
+    }
+    const unsigned long long wi = wave_incl_scan_u64(run);
+    mx = wave_max_u32(mx);
+    if (lane == kWave - 1) wsum[w] = wi;
+    if (lane == 0) wmax[w] = mx;
+    __syncthreads();
+    unsigned long long wpre = 0, agg = 0;
+    for (int k = 0; k < kScanThreads / kWave; ++k) {
+        const unsigned long long x = wsum[k];
+        wpre += k < w ? x : 0ull;
+        agg += x;
+    }
+    if (t == 0) {
+        uint32_t m = 0;
+        for (int k = 0; k < kScanThreads / kWave; ++k) m = max(m, wmax[k]);
+        // max row first (its result waited for), then the status: the max is in place once any
+        // later tile sees this tile's status
+        pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
+        unsigned long long excl = 0;
+        if (tile == 0) {
+            st(&status[0], tag | kStInc | agg);
+        } else {
+            st(&status[tile], tag | kStAgg | agg);
+            for (uint64_t j = tile - 1;; --j) {
+                unsigned long long x;
+                do {
+                    x = ld(&status[j]);
+                } while ((x >> 42) != epoch || (x & (kStAgg | kStInc)) == 0);
+                excl += x & kStVal;
+                if (x & kStInc) break;
+            }
+            st(&status[tile], tag | kStInc | (excl + agg));
+        }
+        s_bcast[1] = excl;
+        if (tile == ntiles - 1) {
+            if (n > 0) rp[0] = 0;
+            const unsigned long long mw = ld(maxw);
+            const unsigned long long out[2] = {excl + agg, (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull};
+            for (int k = 0; k < 2; ++k)
+                __hip_atomic_store(&host_out[k], out[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t m = 0, d = 0;
-        for (int w = 0; w < kWpb; ++w) {
-            m = max(m, red[0][w]);
-            d += red[1][w];
-        }
-        unsigned long long *sh = p.shards + (blockIdx.x % kShards) * kShardStride;
-        if (m) atomicMax(&sh[1], (unsigned long long)m);
-        if (d) atomicAdd(&sh[2], (unsigned long long)d);
-    }
+    const unsigned long long pre = s_bcast[1] + wpre + (wi - run);
+#pragma unroll
+    for (int e = 0; e < kScanItems; ++e)
+        if (i0 + e < n) rp[1 + i0 + e] = pre + v[e];
 }
 
 // ------------------------------------------------------------------------------------------------
