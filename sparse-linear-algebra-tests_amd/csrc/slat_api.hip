@@ -42,6 +42,8 @@ struct slat_ctx {
     uint64_t status_cap = 0;                 // tiles d_status holds
     unsigned long long ticket_base = 0;      // tiles handed out so far (the ticket is monotonic)
     uint32_t scan_epoch = 0;                 // tag of the status / max-row words (22 bits)
+    size_t free_b = 0;                       // cached hipMemGetInfo free bytes
+    uint32_t free_age = 0;
     hipEvent_t ev[6] = {};
     slat_stats stats = {};
 };
@@ -330,6 +332,11 @@ static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hi
 // record in the workspace is indexed by resident wave)
 template <typename Sem>
 static int numeric_blocks_per_cu(bool idx32, bool ell, size_t lds) {
+    // cached per (instance, LDS size): the query costs microseconds of host time per call
+    static thread_local int cache_nb[4] = {0, 0, 0, 0};
+    static thread_local size_t cache_lds[4] = {0, 0, 0, 0};
+    const int ci = (idx32 ? 1 : 0) | (ell ? 2 : 0);
+    if (cache_lds[ci] == lds && cache_nb[ci] > 0) return cache_nb[ci];
     int nb = 0;
     hipError_t e;
     if (idx32 && ell)
@@ -340,7 +347,10 @@ static int numeric_blocks_per_cu(bool idx32, bool ell, size_t lds) {
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint64_t, true>, kBlock, lds);
     else
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint64_t, false>, kBlock, lds);
-    return (e == hipSuccess && nb > 0) ? nb : 1;
+    nb = (e == hipSuccess && nb > 0) ? nb : 1;
+    cache_lds[ci] = lds;
+    cache_nb[ci] = nb;
+    return nb;
 }
 
 static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
@@ -541,9 +551,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
     const unsigned __int128 dense = (unsigned __int128)n * ncols;
     if (bound128 > dense) bound128 = dense;
-    size_t free_b = 0, total_b = 0;
-    (void)hipMemGetInfo(&free_b, &total_b);
-    const unsigned __int128 budget = (unsigned __int128)free_b / 4;
+    // free device memory, refreshed every 32 calls (the query costs host time on every call)
+    if (ctx->free_age++ % 32 == 0) {
+        size_t total_b = 0;
+        (void)hipMemGetInfo(&ctx->free_b, &total_b);
+    }
+    const unsigned __int128 budget = (unsigned __int128)ctx->free_b / 4;
     const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
     if (!exact) {
         C->capacity = (uint64_t)std::max<unsigned __int128>(bound128, 1);

@@ -1053,11 +1053,11 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
 
 // ------------------------------------------------------------------------------------------------
 // row_ptr = inclusive scan of the row counts: ONE single-pass kernel (decoupled look-back). Tiles of
-// 8192 rows are taken in ticket order (a monotonic counter, so no reset), each publishes its
+// 2048 rows are taken in ticket order (a monotonic counter, so no reset), each publishes its
 // aggregate then its inclusive prefix in an epoch-tagged status word (no init kernel). The last
 // tile writes the total nnz and the max row nnz into mapped host memory (no copy in the stream).
 // ------------------------------------------------------------------------------------------------
-constexpr int kScanThreads = 1024, kScanItems = 8;
+constexpr int kScanThreads = 256, kScanItems = 8;
 constexpr uint64_t kScanTile = (uint64_t)kScanThreads * kScanItems;
 constexpr unsigned long long kStAgg = 1ull << 40, kStInc = 2ull << 40, kStVal = (1ull << 40) - 1;
 
