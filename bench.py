@@ -103,13 +103,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one rank per GPU; SLAT_DIST_BACKEND=gloo rehearses the multi-rank flow with ranks sharing the
+    # visible GPU(s) (the metric's runs use RCCL, "nccl")
+    backend = os.environ.get("SLAT_DIST_BACKEND", "nccl")
+    dev_index = local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dev_index = local % max(1, torch.cuda.device_count())
+            dist.init_process_group(backend)
+    coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
 
-    ctx = slat.Context(local)
+    ctx = slat.Context(dev_index)
     side, power = args.side, args.power
     if args.scaling == "strong" and world > 1 and side == 30:
         side, power = 100, 4
@@ -157,10 +166,10 @@ def main():
     units = nnz_c * args.steps
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        u = torch.tensor([units], dtype=torch.float64, device=f"cuda:{local}")
+        u = torch.tensor([units], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         units = int(u.item())
 
@@ -175,8 +184,9 @@ def main():
         hc = C.host()
         dist.barrier()
         tg = time.perf_counter()
-        slat_dist.gather_blocks(hc.row_ptr, hc.col_idx, hc.values, device=torch.device("cuda", local))
-        torch.cuda.synchronize()
+        slat_dist.gather_blocks(hc.row_ptr, hc.col_idx, hc.values, device=torch.device(coll_dev))
+        if backend == "nccl":
+            torch.cuda.synchronize()
         dist.barrier()
         gather_ms = (time.perf_counter() - tg) * 1e3
         del C
