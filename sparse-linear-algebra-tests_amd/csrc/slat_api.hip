@@ -405,22 +405,19 @@ static slat_status launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n
 }
 
 
-// Window geometry for a group of `threads` lanes: ww = threads * per with `per` odd (thread-
-// contiguous word ownership is then free of LDS bank conflicts) and ww <= max_ww (u16 ranks need
-// 32 * ww <= 65536). `wide` = one window does not cover all columns.
+// Window geometry: ww bitmap words, a multiple of 64 (words are handled in 64-word blocks, one word
+// per lane) and at most max_ww (u16 column offsets need 32 * ww <= 65536; the touched-block mask
+// needs ww / 64 <= 32). `wide` = one window does not cover all columns.
 static void pick_window(uint64_t ncols, uint32_t threads, uint32_t max_ww, uint32_t &ww, uint32_t &wide) {
-    const uint64_t words = (ncols + 31) / 32;
-    uint64_t per = (words + threads - 1) / threads;
-    if (per == 0) per = 1;
-    if ((per & 1) == 0) per += 1;
-    uint64_t max_per = max_ww / threads;
-    if ((max_per & 1) == 0) max_per -= 1;
+    const uint64_t words = std::max<uint64_t>((ncols + 31) / 32, 1);
+    uint64_t blocks = (words + threads - 1) / threads;
+    const uint64_t max_blocks = max_ww / threads;
     wide = 0;
-    if (per > max_per) {
-        per = max_per;
+    if (blocks > max_blocks) {
+        blocks = max_blocks;
         wide = 1;
     }
-    ww = (uint32_t)(per * threads);
+    ww = (uint32_t)(blocks * threads);
 }
 
 extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,

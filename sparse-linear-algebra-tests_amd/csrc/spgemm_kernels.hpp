@@ -200,6 +200,9 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return readlane_u32(wave_incl_scan(v, 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return min(a, b); }), kWave - 1);
 }
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+    return readlane_u32(wave_incl_scan(v, 0u, [](uint32_t a, uint32_t b) { return a | b; }), kWave - 1);
+}
 __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t x) {
     return wave_incl_scan(x, 0u, [](uint32_t a, uint32_t b) { return a + b; }) - x;
 }
@@ -723,12 +726,16 @@ template <typename S, int STRIDE = 2>
 struct BitmapPass {
     uint32_t *L0;
     uint32_t wlo, WIN;
+    uint32_t blk = 0;  // lane's mask of touched 64-word blocks (2048 columns each)
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &) {
         const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             uint32_t off;
-            if (win_off(cc[e], wlo, WIN, off)) atomicOr(&L0[(off >> 5) * STRIDE], 1u << (off & 31));
+            if (win_off(cc[e], wlo, WIN, off)) {
+                atomicOr(&L0[(off >> 5) * STRIDE], 1u << (off & 31));
+                blk |= 1u << (off >> 11);
+            }
         }
     }
     __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
@@ -824,8 +831,6 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     for (uint32_t w = lane; w < p.ww; w += kWave) L0[w] = 0;
     wave_sync();
     const uint32_t WIN = p.ww * 32;
-    const uint32_t per = p.ww / kWave;  // odd: lane-contiguous word ownership is conflict-free
-    const uint32_t wb0 = lane * per;
     unsigned long long flops = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     for (uint64_t row = (uint64_t)blockIdx.x * kWpb + wv; row < p.nrows; row += stride) {
@@ -850,11 +855,13 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
                 SymPass<1> sp{BitmapPass<uint32_t, 1>{L0, (uint32_t)wlo, WIN}, p.stats != 0 && first};
                 if (!(p.ablate & 1u)) rw.template each_group<false>(sp);
                 wave_sync();
-                // count = popcount of the window; lane owns words [wb0, wb0 + per) and clears them
+                // count = popcount of the touched 64-word blocks only (word b*64 + lane per lane),
+                // which the same lanes then clear
                 uint32_t lc = 0;
-                for (uint32_t q = 0; q < per; ++q) {
-                    lc += __popc(L0[wb0 + q]);
-                    L0[wb0 + q] = 0;
+                for (uint32_t m = wave_or_u32(sp.bm.blk); m; m &= m - 1) {
+                    const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
+                    lc += __popc(L0[w]);
+                    L0[w] = 0;
                 }
                 cnt += wave_sum_u32(lc);
                 if (first && p.stats) flops += wave_sum_u32(sp.nprod);
@@ -902,8 +909,6 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     wave_sync();
 
     const uint32_t WIN = p.ww * 32;
-    const uint32_t per = p.ww / kWave;  // odd: lane-contiguous word ownership is conflict-free
-    const uint32_t wb0 = lane * per;
     uint32_t zrows = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     PhaseClock pc{};
@@ -942,19 +947,18 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 wave_sync();
                 (void)__builtin_amdgcn_readfirstlane(L0[0]);
                 mark(1);  // bitmap pass
-                // 2. word ranks (lane owns words [wb0, wb0 + per)) into W[w].y
-                uint32_t lc = 0;
-                for (uint32_t q = 0; q < per; ++q) lc += __popc(W[wb0 + q].x);
-                const uint32_t ex = wave_excl_scan_u32(lc);
-                const uint32_t wcnt = readlane_u32(ex + lc, kWave - 1);
-                if (wcnt == 0) continue;  // bitmap empty: nothing to clear
-                {
-                    uint32_t run = ex;
-                    for (uint32_t q = 0; q < per; ++q) {
-                        W[wb0 + q].y = run;
-                        run += __popc(W[wb0 + q].x);
-                    }
+                // 2. word ranks into W[w].y, over the touched 64-word blocks only: block b's words are
+                //    b*64 + lane, a wave scan per block carried across blocks
+                const uint32_t bmask = wave_or_u32(bm.blk);
+                uint32_t wcnt = 0;
+                for (uint32_t m = bmask; m; m &= m - 1) {
+                    const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
+                    const uint32_t c = __popc(W[w].x);
+                    const uint32_t incl = wave_incl_scan(c, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+                    W[w].y = wcnt + incl - c;
+                    wcnt += readlane_u32(incl, kWave - 1);
                 }
+                if (wcnt == 0) continue;  // bitmap empty: nothing to clear
                 mark(2);  // word ranks
                 // narrow u32 slots when the row's sums provably stay below 2^32:
                 // max(A row) * max(B) * len(A row) < 2^32 (each output sums <= len products)
@@ -1029,7 +1033,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 } else {
                     run_chunks(std::false_type{});
                 }
-                for (uint32_t q = 0; q < per; ++q) W[wb0 + q].x = 0;
+                for (uint32_t m = bmask; m; m &= m - 1) W[(uint32_t)__builtin_ctz(m) * kWave + lane].x = 0;
                 wave_sync();
             }
         }
