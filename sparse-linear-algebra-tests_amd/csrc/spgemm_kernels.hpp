@@ -43,6 +43,8 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 constexpr int kShards = 64;      // sharded status words (avoid one hot atomic address)
 constexpr uint32_t kSent = 0xFFFFFFFFu;  // ELL padding (column ids are < n_cols <= 2^32 - 1)
+// words of the B-value summary block (context memory, epoch-tagged): max B value, ~min B value
+constexpr int kVMaxWord = 0, kVMinInvWord = 3;
 constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2] rows with zeros, [3] flops
 
 #ifndef SLAT_PHASES
@@ -81,7 +83,8 @@ struct Args {
     const uint32_t *ell_col;  // [n_B][ell_wq*4] columns, kSent padded
     const void *ell_val;      // [n_B][ell_wq*4] values
     const uint8_t *ell_ng;    // [n_B] groups of 4 holding real entries: ceil(len / 4)
-    unsigned long long *b_vmax;  // (epoch << 32) | max B value, from k_build_ell (u32 only; else null)
+    unsigned long long *b_vmax;  // B-value summary from k_build_ell (u32 only; else null): [kVMaxWord]
+                                 // (epoch << 32) | max, [kVMinInvWord] (epoch << 32) | ~min
     uint32_t epoch;
     unsigned long long *host_out;  // mapped pinned host words: [0] nnz, [1] max row nnz, [2] rows with zeros
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
                                                        uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng,
                                                        unsigned long long *vmax, uint32_t epoch) {
     // one thread per (row k, group t): 4 columns and 4 values, written as whole groups
-    uint32_t mx = 0;
+    uint32_t mx = 0, mn = 0xFFFFFFFFu;
     const uint64_t total = (uint64_t)n * wq;
     for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (uint64_t)gridDim.x * kBlock) {
         const uint64_t k = g / wq;
@@ -276,22 +279,33 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
             c[e] = u < len ? col[s0 + u] : kSent;
             v[e] = u < len ? val[s0 + u] : S(0);
             if constexpr (std::is_same<S, uint32_t>::value)
-                if (u < len) mx = max(mx, (uint32_t)v[e]);
+                if (u < len) {
+                    mx = max(mx, (uint32_t)v[e]);
+                    mn = min(mn, (uint32_t)v[e]);
+                }
         }
         ((uint4 *)ecol)[g] = make_uint4(c[0], c[1], c[2], c[3]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) eval[g * 4 + e] = v[e];
     }
     if constexpr (std::is_same<S, uint32_t>::value) {
-        // max B value, one atomic per block; the epoch in the high word supersedes earlier calls'
-        // values without a reset
-        __shared__ uint32_t bm[kBlock / kWave];
+        // max and min B value, one atomic each per block (the min as max of ~v); the epoch in the
+        // high word supersedes earlier calls' values without a reset
+        __shared__ uint32_t bm[kBlock / kWave], bn[kBlock / kWave];
         mx = wave_max_u32(mx);
-        if (lane_id() == 0) bm[threadIdx.x / kWave] = mx;
+        mn = wave_min_u32(mn);
+        if (lane_id() == 0) {
+            bm[threadIdx.x / kWave] = mx;
+            bn[threadIdx.x / kWave] = mn;
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
-            for (int w = 1; w < kBlock / kWave; ++w) mx = max(mx, bm[w]);
-            atomicMax(vmax, ((unsigned long long)epoch << 32) | mx);
+            for (int w = 1; w < kBlock / kWave; ++w) {
+                mx = max(mx, bm[w]);
+                mn = min(mn, bn[w]);
+            }
+            atomicMax(&vmax[kVMaxWord], ((unsigned long long)epoch << 32) | mx);
+            atomicMax(&vmax[kVMinInvWord], ((unsigned long long)epoch << 32) | ~mn);
         }
     }
 }
@@ -340,6 +354,14 @@ template <typename S>
 __device__ __forceinline__ Quad<S> quad1(S v) {
     Quad<S> q{};
     q.v[0] = v;
+    return q;
+}
+
+template <typename S>
+__device__ __forceinline__ Quad<S> splat4(S v) {
+    Quad<S> q;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q.v[e] = v;
     return q;
 }
 
@@ -650,9 +672,11 @@ struct RowWalker {
         if (nb > kNB) nb = kOvf;
     }
 
-    // grp(c4, pr4) / grp.multi(c4[kRegQ], pr4[kRegQ]) for every group; products (PSem) when VV
-    template <bool VV, typename PSem = Sem, typename G>
-    __device__ __forceinline__ void each_group(G &grp) {
+    // grp(c4, pr4) / grp.multi(c4[kRegQ], pr4[kRegQ]) for every group; products (PSem) when VV.
+    // UNI: every B value equals v0 (a pattern B), so no B values are loaded and an entry's four
+    // products are the one value prod(a, v0)
+    template <bool VV, typename PSem = Sem, bool UNI = false, typename G>
+    __device__ __forceinline__ void each_group(G &grp, S v0 = S(0)) {
         if constexpr (ELL) {
             for (uint32_t sg = 0; sg < nseg; ++sg) {
                 if (!single) load_seg(a0 + (I)((uint64_t)sg * kSeg));
@@ -670,18 +694,22 @@ struct RowWalker {
                     pq[q] = Quad<S>{};
                     if (kq[q] != kSent) {
                         cq[q] = ell_cols(p, kq[q], 0);
-                        if constexpr (VV) pq[q] = ell_vals<S>(p, kq[q], 0);
+                        if constexpr (VV && !UNI) pq[q] = ell_vals<S>(p, kq[q], 0);
                     }
                 });
                 if (bk0 != kSent) {
                     ct0 = ell_cols(p, bk0, bt0);
-                    if constexpr (VV) pt0 = ell_vals<S>(p, bk0, bt0);
+                    if constexpr (VV && !UNI) pt0 = ell_vals<S>(p, bk0, bt0);
                 }
                 if (bk1 != kSent) {
                     ct1 = ell_cols(p, bk1, bt1);
-                    if constexpr (VV) pt1 = ell_vals<S>(p, bk1, bt1);
+                    if constexpr (VV && !UNI) pt1 = ell_vals<S>(p, bk1, bt1);
                 }
-                if constexpr (VV) {
+                if constexpr (VV && UNI) {
+                    sfor<kRegQ>([&](auto Q) { pq[Q] = splat4(PSem::prod(aq[Q], v0)); });
+                    pt0 = splat4(PSem::prod(ba0, v0));
+                    pt1 = splat4(PSem::prod(ba1, v0));
+                } else if constexpr (VV) {
                     sfor<kRegQ>([&](auto Q) { pq[Q] = prods<PSem>(aq[Q], pq[Q]); });
                     pt0 = prods<PSem>(ba0, pt0);
                     pt1 = prods<PSem>(ba1, pt1);
@@ -721,8 +749,8 @@ struct SpanPass {
 };
 
 // the window's column bitmap: word w at L0[w * STRIDE] (numeric: W[w].x, STRIDE 2; symbolic: 1),
-// fire-and-forget LDS atomics
-template <typename S, int STRIDE = 2>
+// fire-and-forget LDS atomics. Z: the window starts at column 0 (one window covers every column).
+template <typename S, int STRIDE = 2, bool Z = false>
 struct BitmapPass {
     uint32_t *L0;
     uint32_t wlo, WIN;
@@ -732,7 +760,7 @@ struct BitmapPass {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             uint32_t off;
-            if (win_off(cc[e], wlo, WIN, off)) {
+            if (win_off(cc[e], Z ? 0u : wlo, WIN, off)) {
                 atomicOr(&L0[(off >> 5) * STRIDE], 1u << (off & 31));
                 blk |= 1u << (off >> 11);
             }
@@ -745,7 +773,9 @@ struct BitmapPass {
 
 // numeric pass 3: accumulate products into rank slots; all rank lookups of a batch first.
 // NARROW: u32 value slots (the row provably cannot reach 2^32), else the semiring's V slots.
-template <typename Sem, bool NARROW>
+// Z: the window starts at column 0; R0: the chunk starts at rank 0 (the window's ranks fit one
+// chunk); UNI: a group's four products are one value (pattern B). Each drops per-slot VALU work.
+template <typename Sem, bool NARROW, bool Z = false, bool R0 = false, bool UNI = false>
 struct AccPass {
     using S = typename Sem::S;
     const uint2 *W;
@@ -760,17 +790,20 @@ struct AccPass {
         S pr[Q][4];
         // products pinned in VGPRs up front: keeps B-value loads out of the per-slot branches
 #pragma unroll
-        for (int q = 0; q < Q; ++q)
+        for (int q = 0; q < Q; ++q) {
+            S u = pr_in[q].v[0];
+            if constexpr (UNI) pin(u);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                pr[q][e] = pr_in[q].v[e];
-                pin(pr[q][e]);
+                pr[q][e] = UNI ? u : pr_in[q].v[e];
+                if constexpr (!UNI) pin(pr[q][e]);
             }
+        }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             const uint32_t cc[4] = {c[q].x, c[q].y, c[q].z, c[q].w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) w[q][e] = rank_word(W, ww, cc[e], wlo, off[q][e]);
+            for (int e = 0; e < 4; ++e) w[q][e] = rank_word(W, ww, cc[e], Z ? 0u : wlo, off[q][e]);
         }
         if constexpr (SLAT_PHASES) {
             pin(w[0][0].x);
@@ -780,7 +813,7 @@ struct AccPass {
         for (int q = 0; q < Q; ++q) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const uint32_t r = rank_in(w[q][e], off[q][e], r0, nch);
+                const uint32_t r = rank_in(w[q][e], off[q][e], R0 ? 0u : r0, nch);
                 if (r != kSent) {
                     if constexpr (NARROW)
                         atomicAdd((uint32_t *)vals + r, (uint32_t)pr[q][e]);
@@ -897,11 +930,17 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     // rank-chunk capacities: narrow = u32 value + u16 column, wide = V*kSlots + u16 column
     const uint32_t cap_n = p.area / 6, cap_w = p.area / (uint32_t)(sizeof(V) * Sem::kSlots + 2);
     uint32_t bvmax = 0xFFFFFFFFu;  // max B value of this call (u32 semiring with the ELL copy)
+    bool buni = false;             // every B value equals bvmax (a pattern B)
     if constexpr (Sem::kNarrowable)
-        if (p.b_vmax) {
-            const unsigned long long v = *(volatile unsigned long long *)p.b_vmax;
-            if ((uint32_t)(v >> 32) == p.epoch) bvmax = (uint32_t)v;
+        if (ELL && p.b_vmax) {
+            const unsigned long long v = ((volatile unsigned long long *)p.b_vmax)[kVMaxWord];
+            const unsigned long long vi = ((volatile unsigned long long *)p.b_vmax)[kVMinInvWord];
+            if ((uint32_t)(v >> 32) == p.epoch) {
+                bvmax = (uint32_t)v;
+                buni = (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax;
+            }
         }
+    const S bv0 = (S)bvmax;
     S *cval = (S *)p.c_val;
 
     for (uint32_t w = lane; w < p.ww; w += kWave) W[w] = make_uint2(0u, 0u);
@@ -939,10 +978,11 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                     hi = 0;
                 }
             }
-            for (uint64_t wlo64 = lo & ~31ull; wlo64 <= hi; wlo64 += WIN) {
-                const uint32_t wlo = (uint32_t)wlo64;
+            // one window: Z (std::true_type) when it starts at column 0 and covers every column
+            auto window = [&](auto ztag, uint32_t wlo) {
+                constexpr bool Z = decltype(ztag)::value;
                 // 1. column bitmap of the window (into W[w].x)
-                BitmapPass<S> bm{L0, wlo, WIN};
+                BitmapPass<S, 2, Z> bm{L0, wlo, WIN};
                 if (!(p.ablate & 32u)) each_group(bm, std::false_type{});
                 wave_sync();
                 (void)__builtin_amdgcn_readfirstlane(L0[0]);
@@ -958,7 +998,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                     W[w].y = wcnt + incl - c;
                     wcnt += readlane_u32(incl, kWave - 1);
                 }
-                if (wcnt == 0) continue;  // bitmap empty: nothing to clear
+                if (wcnt == 0) return;  // bitmap empty: nothing to clear
                 mark(2);  // word ranks
                 // narrow u32 slots when the row's sums provably stay below 2^32:
                 // max(A row) * max(B) * len(A row) < 2^32 (each output sums <= len products)
@@ -969,72 +1009,88 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                         narrow = x == 0 || len <= 0xFFFFFFFFull / x;
                     }
                 }
-                auto run_chunks = [&](auto narrow_tag) {
+                // one rank chunk [r0, r0 + nch): zero its slots, accumulate, emit. R0: r0 == 0.
+                auto chunk = [&](auto narrow_tag, auto uni_tag, auto r0tag, uint32_t r0, uint32_t cap) {
                     constexpr bool NW = decltype(narrow_tag)::value;
+                    constexpr bool UNI = decltype(uni_tag)::value;
+                    constexpr bool R0 = decltype(r0tag)::value;
                     using VS = std::conditional_t<NW, uint32_t, V>;  // value slot word
                     constexpr uint32_t kVW = NW ? 1 : Sem::kSlots;   // words per slot
-                    const uint32_t cap = NW ? cap_n : cap_w;
                     VS *vals = (VS *)slots;
                     uint16_t *cols = (uint16_t *)(slots + ((cap * kVW * sizeof(VS) + 3) & ~3u));
-                    for (uint32_t r0 = 0; r0 < wcnt; r0 += cap) {
-                        const uint32_t nch = min(cap, wcnt - r0);
-                        for (uint32_t t = lane; t < nch * kVW; t += kWave) vals[t] = VS(0);
-                        wave_sync();
-                        mark(8);  // zero value slots
-                        // 3. values and the column offset of every rank (duplicates store the same)
-                        if constexpr (Sem::kOrdered) {
-                            if (!(p.ablate & 8u))
-                                traverse_ordered<I, S>(p, a0, a1, [&](uint32_t j, S a, S b) {
-                                    uint32_t off;
-                                    const uint2 w = rank_word(W, p.ww, j, wlo, off);
-                                    const uint32_t r = rank_in(w, off, r0, nch);
-                                    if (r != kSent) {
-                                        Sem::acc((V *)vals, r, Sem::prod(a, b));
-                                        cols[r] = (uint16_t)off;
-                                    }
-                                });
-                        } else if (!(p.ablate & 8u)) {
-                            AccPass<Sem, NW> acc{W, vals, cols, p.ww, wlo, r0, nch, &pc};
-                            if constexpr (NW)
-                                rw.template each_group<true, SemU32Narrow>(acc);
-                            else
-                                rw.template each_group<true>(acc);
+                    const uint32_t nch = min(cap, wcnt - r0);
+                    for (uint32_t t = lane; t < nch * kVW; t += kWave) vals[t] = VS(0);
+                    wave_sync();
+                    mark(8);  // zero value slots
+                    // 3. values and the column offset of every rank (duplicates store the same)
+                    if constexpr (Sem::kOrdered) {
+                        if (!(p.ablate & 8u))
+                            traverse_ordered<I, S>(p, a0, a1, [&](uint32_t j, S a, S b) {
+                                uint32_t off;
+                                const uint2 w = rank_word(W, p.ww, j, wlo, off);
+                                const uint32_t r = rank_in(w, off, r0, nch);
+                                if (r != kSent) {
+                                    Sem::acc((V *)vals, r, Sem::prod(a, b));
+                                    cols[r] = (uint16_t)off;
+                                }
+                            });
+                    } else if (!(p.ablate & 8u)) {
+                        AccPass<Sem, NW, Z && R0, Z && R0, UNI> acc{W, vals, cols, p.ww, wlo, r0, nch, &pc};
+                        if constexpr (NW)
+                            rw.template each_group<true, SemU32Narrow, UNI>(acc, bv0);
+                        else
+                            rw.template each_group<true, Sem, UNI>(acc, bv0);
+                    }
+                    wave_sync();
+                    if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
+                    mark(12);  // accumulate pass drain
+                    // 4. emit at the row's slice, coalesced
+                    // wave-uniform output base + 32-bit lane offsets
+                    uint32_t *oc = p.c_col + out_pos;
+                    S *ov = cval + out_pos;
+                    const uint32_t lim = (uint32_t)min<uint64_t>(out_end - min(out_pos, out_end), nch);
+                    for (uint32_t t = lane; t < nch; t += kWave) {
+                        S v;
+                        if constexpr (NW)
+                            v = (S)vals[t];
+                        else
+                            v = Sem::finish((const V *)vals, t);
+                        zeros += Sem::is_zero(v) ? 1u : 0u;
+                        if (t < lim && !(p.ablate & 16u)) {  // never write past the row's slice
+                            oc[t] = wlo + cols[t];
+                            ov[t] = v;
                         }
-                        wave_sync();
-                        if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
-                        mark(12);  // accumulate pass drain
-                        // 4. emit at the row's slice, coalesced
-                        // wave-uniform output base + 32-bit lane offsets
-                        uint32_t *oc = p.c_col + out_pos;
-                        S *ov = cval + out_pos;
-                        const uint32_t lim = (uint32_t)min<uint64_t>(out_end - min(out_pos, out_end), nch);
-                        for (uint32_t t = lane; t < nch; t += kWave) {
-                            S v;
-                            if constexpr (NW)
-                                v = (S)vals[t];
-                            else
-                                v = Sem::finish((const V *)vals, t);
-                            zeros += Sem::is_zero(v) ? 1u : 0u;
-                            if (t < lim && !(p.ablate & 16u)) {  // never write past the row's slice
-                                oc[t] = wlo + cols[t];
-                                ov[t] = v;
-                            }
-                        }
-                        out_pos += nch;
-                        wave_sync();
-                        mark(4);  // emit
+                    }
+                    out_pos += nch;
+                    wave_sync();
+                    mark(4);  // emit
+                };
+                auto run_chunks = [&](auto narrow_tag, auto uni_tag) {
+                    constexpr bool NW = decltype(narrow_tag)::value;
+                    const uint32_t cap = NW ? cap_n : cap_w;
+                    if (Z && wcnt <= cap) {  // the common case: one chunk from rank 0
+                        chunk(narrow_tag, uni_tag, std::true_type{}, 0u, cap);
+                    } else {
+                        for (uint32_t r0 = 0; r0 < wcnt; r0 += cap) chunk(narrow_tag, uni_tag, std::false_type{}, r0, cap);
                     }
                 };
-                if constexpr (Sem::kNarrowable) {
-                    if (narrow)
-                        run_chunks(std::true_type{});
+                if constexpr (Sem::kNarrowable && ELL) {
+                    if (narrow && buni)
+                        run_chunks(std::true_type{}, std::true_type{});
+                    else if (narrow)
+                        run_chunks(std::true_type{}, std::false_type{});
                     else
-                        run_chunks(std::false_type{});
+                        run_chunks(std::false_type{}, std::false_type{});
                 } else {
-                    run_chunks(std::false_type{});
+                    run_chunks(std::false_type{}, std::false_type{});
                 }
                 for (uint32_t m = bmask; m; m &= m - 1) W[(uint32_t)__builtin_ctz(m) * kWave + lane].x = 0;
                 wave_sync();
+            };
+            if (!p.wide) {
+                window(std::true_type{}, 0u);
+            } else {
+                for (uint64_t wlo64 = lo & ~31ull; wlo64 <= hi; wlo64 += WIN) window(std::false_type{}, (uint32_t)wlo64);
             }
         }
         mark(5);  // window clears, empty rows

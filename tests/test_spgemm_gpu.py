@@ -153,6 +153,31 @@ def test_u32_narrow_slot_bound(ctx, k):
         assert want.get(0, 0) == 0xFFFFFFFF
 
 
+@pytest.mark.parametrize("v0", [7, 0, 0xFFFFFFFF])
+def test_u32_pattern_b(ctx, v0):
+    # Every B value equal (a pattern B, as the torus chain's B = A): the kernel skips the B-value
+    # loads and forms one product a * v0 per A entry. v0 = 0: every product is zero and every row
+    # drops out; v0 = 2^32 - 1: the rows are not narrow (the u64-slot, saturating path).
+    rng = np.random.default_rng(11)
+    n = 3000
+    ar = np.repeat(np.arange(n), 24)
+    ac = rng.integers(0, n, len(ar))
+    av = rng.integers(1, 1000, len(ar)).astype(np.uint64)
+    a = O.from_coo(n, ar, ac, av, O.U32)
+    br = np.repeat(np.arange(n), 9)
+    bc = rng.integers(0, n, len(br))
+    if v0 == 0:
+        # explicit zeros only enter through raw arrays (the COO builders drop them)
+        rp, col, _ = O.from_coo(n, br, bc, np.ones(len(br), np.uint64), O.U32).arrays()
+        B = slat.CsrMatrix.from_host(slat.HostCsr(n, rp, col, np.zeros(len(col), np.uint32), slat.U32))
+        h = to_dev(a, slat.U32)._spgemm(B).host()
+        assert len(h.col_idx) == 0
+        np.testing.assert_array_equal(h.row_ptr, np.zeros(n + 1, np.uint64))
+        return
+    b = O.from_coo(n, br, bc, np.full(len(br), v0, np.uint64), O.U32)
+    assert_same(to_dev(a, slat.U32)._spgemm(to_dev(b, slat.U32)), O.matmul_seq(a, b), f"pattern B v0={v0}")
+
+
 # ---- f64 (config C5 shape, small): bit-exact left fold ----
 def test_f64_rmat_bit_exact(ctx):
     h = slat.host_rmat(12, 40000)
