@@ -525,9 +525,19 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const size_t shards_b = 4096 + (SLAT_PHASES ? 8192 : 0);  // + phase-timing slots (diagnostic builds)
     const size_t ecol_b = ell ? up256(B->n_rows * wq * 16) : 0, eval_b = ell ? up256(B->n_rows * wq * 4 * vs) : 0;
     const size_t eng_b = ell ? up256(B->n_rows) : 0;
+    // stored bitmaps (single-window launches): symbolic keeps each row's touched bitmap blocks for
+    // numeric, n * ww words at most (only touched blocks are written), capped against free memory
+    if (ctx->free_age++ % 32 == 0) {
+        size_t total_b = 0;
+        (void)hipMemGetInfo(&ctx->free_b, &total_b);
+    }
+    const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
+    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) &&
+                     !std::getenv("SLAT_NO_SBM");
+    const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
-                 o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b;
-    if ((st = ensure_ws(ctx, o_eng + eng_b))) return st;
+                 o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
+    if ((st = ensure_ws(ctx, o_smask + smask_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (ell) {
         a.ell_wq = (uint32_t)wq;
@@ -541,6 +551,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     a.counts = (uint64_t *)ws;
     a.shards = (unsigned long long *)(ws + o_sh);
+    if (sbm) {
+        a.sbm = (uint32_t *)(ws + o_sbm);
+        a.smask = (uint32_t *)(ws + o_smask);
+        a.nblk = a.ww / kWave;
+    }
     a.host_out = ctx->h_out_dev;
     ctx->h_out[0] = ctx->h_out[1] = ctx->h_out[2] = 0;  // no kernel of this context is in flight
 
@@ -548,11 +563,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
     const unsigned __int128 dense = (unsigned __int128)n * ncols;
     if (bound128 > dense) bound128 = dense;
-    // free device memory, refreshed every 32 calls (the query costs host time on every call)
-    if (ctx->free_age++ % 32 == 0) {
-        size_t total_b = 0;
-        (void)hipMemGetInfo(&ctx->free_b, &total_b);
-    }
+    // free device memory: refreshed every 32 calls above (the query costs host time on every call)
     const unsigned __int128 budget = (unsigned __int128)ctx->free_b / 4;
     const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
     if (!exact) {
@@ -573,6 +584,9 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     asym.ell_col = a.ell_col;
     asym.ell_val = a.ell_val;
     asym.ell_ng = a.ell_ng;
+    asym.sbm = a.sbm;
+    asym.smask = a.smask;
+    asym.nblk = a.nblk;
     if (ell) {
         hipError_t be;
         if (dt == SLAT_U32)

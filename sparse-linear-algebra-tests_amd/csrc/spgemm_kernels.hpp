@@ -86,6 +86,12 @@ struct Args {
     unsigned long long *b_vmax;  // B-value summary from k_build_ell (u32 only; else null): [kVMaxWord]
                                  // (epoch << 32) | max, [kVMinInvWord] (epoch << 32) | ~min
     uint32_t epoch;
+    // stored bitmaps (single-window launches, else null): symbolic keeps row r's touched 64-word
+    // blocks at sbm[r * nblk * 64 + w] and their mask at smask[r]; numeric loads them instead of
+    // rebuilding the bitmap
+    uint32_t *sbm;
+    uint32_t *smask;
+    uint32_t nblk;
     unsigned long long *host_out;  // mapped pinned host words: [0] nnz, [1] max row nnz, [2] rows with zeros
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
@@ -833,9 +839,9 @@ struct AccPass {
 // symbolic: structural nnz per output row, one wavefront per row (the RowWalker traversal, column
 // bitmap only; counts = popcounts of the lane-owned words, which the same lanes then clear)
 // ------------------------------------------------------------------------------------------------
-template <int STRIDE>
+template <int STRIDE, bool Z = false>
 struct SymPass {
-    BitmapPass<uint32_t, STRIDE> bm;
+    BitmapPass<uint32_t, STRIDE, Z> bm;
     bool count;
     uint32_t nprod = 0;
     __device__ __forceinline__ void operator()(uint4 c, const Quad<uint32_t> &pr) {
@@ -884,22 +890,38 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
                 }
             }
             bool first = true;
-            for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) {
-                SymPass<1> sp{BitmapPass<uint32_t, 1>{L0, (uint32_t)wlo, WIN}, p.stats != 0 && first};
+            // one window; Z (std::true_type) when it starts at column 0 and covers every column
+            auto window = [&](auto ztag, uint32_t wlo) {
+                constexpr bool Z = decltype(ztag)::value;
+                SymPass<1, Z> sp{BitmapPass<uint32_t, 1, Z>{L0, wlo, WIN}, p.stats != 0 && first};
                 if (!(p.ablate & 1u)) rw.template each_group<false>(sp);
                 wave_sync();
                 // count = popcount of the touched 64-word blocks only (word b*64 + lane per lane),
                 // which the same lanes then clear
                 uint32_t lc = 0;
-                for (uint32_t m = wave_or_u32(sp.bm.blk); m; m &= m - 1) {
+                const uint32_t bmask = wave_or_u32(sp.bm.blk);
+                uint32_t *keep = nullptr;  // the stored bitmap of this row (Z launches with p.sbm)
+                if constexpr (Z)
+                    if (p.sbm) {
+                        keep = p.sbm + row * ((uint64_t)p.nblk * kWave);
+                        if (lane == 0) p.smask[row] = bmask;
+                    }
+                for (uint32_t m = bmask; m; m &= m - 1) {
                     const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
-                    lc += __popc(L0[w]);
+                    const uint32_t x = L0[w];
+                    lc += __popc(x);
                     L0[w] = 0;
+                    if (keep) keep[w] = x;
                 }
                 cnt += wave_sum_u32(lc);
                 if (first && p.stats) flops += wave_sum_u32(sp.nprod);
                 first = false;
                 wave_sync();
+            };
+            if (!p.wide) {
+                window(std::true_type{}, 0u);
+            } else {
+                for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) window(std::false_type{}, (uint32_t)wlo);
             }
         }
         if (lane == 0) p.counts[row] = cnt;
@@ -981,24 +1003,56 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
             // one window: Z (std::true_type) when it starts at column 0 and covers every column
             auto window = [&](auto ztag, uint32_t wlo) {
                 constexpr bool Z = decltype(ztag)::value;
-                // 1. column bitmap of the window (into W[w].x)
-                BitmapPass<S, 2, Z> bm{L0, wlo, WIN};
-                if (!(p.ablate & 32u)) each_group(bm, std::false_type{});
-                wave_sync();
-                (void)__builtin_amdgcn_readfirstlane(L0[0]);
-                mark(1);  // bitmap pass
-                // 2. word ranks into W[w].y, over the touched 64-word blocks only: block b's words are
-                //    b*64 + lane, a wave scan per block carried across blocks
-                const uint32_t bmask = wave_or_u32(bm.blk);
-                uint32_t wcnt = 0;
-                for (uint32_t m = bmask; m; m &= m - 1) {
-                    const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
-                    const uint32_t c = __popc(W[w].x);
-                    const uint32_t incl = wave_incl_scan(c, 0u, [](uint32_t x, uint32_t y) { return x + y; });
-                    W[w].y = wcnt + incl - c;
-                    wcnt += readlane_u32(incl, kWave - 1);
+                const bool stored = Z && p.sbm != nullptr;  // launch-uniform
+                uint32_t bmask, wcnt = 0;
+                if (stored) {
+                    // 1'. the row's bitmap as symbolic left it: touched blocks only, loaded 8 blocks
+                    //     at a time, ranked from registers and written whole ({bits, rank} per word),
+                    //     so untouched blocks may hold stale words (no valid column reads them) and
+                    //     nothing is cleared afterwards
+                    bmask = __builtin_amdgcn_readfirstlane(p.smask[row]);
+                    const uint32_t *src = p.sbm + row * ((uint64_t)p.nblk * kWave) + lane;
+                    for (uint32_t m = bmask; m;) {
+                        uint32_t bs[8], xs[8];
+                        sfor<8>([&](auto I_) {
+                            bs[I_] = m ? (uint32_t)__builtin_ctz(m) : 32u;
+                            m &= m - 1;
+                        });
+                        sfor<8>([&](auto I_) {
+                            xs[I_] = 0;
+                            if (bs[I_] < 32u) xs[I_] = src[bs[I_] * kWave];
+                        });
+                        sfor<8>([&](auto I_) {
+                            if (bs[I_] < 32u) {
+                                const uint32_t c = __popc(xs[I_]);
+                                const uint32_t incl = wave_incl_scan(c, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+                                W[bs[I_] * kWave + lane] = make_uint2(xs[I_], wcnt + incl - c);
+                                wcnt += readlane_u32(incl, kWave - 1);
+                            }
+                        });
+                    }
+                    wave_sync();
+                    mark(1);
+                    if (wcnt == 0) return;
+                } else {
+                    // 1. column bitmap of the window (into W[w].x)
+                    BitmapPass<S, 2, Z> bm{L0, wlo, WIN};
+                    if (!(p.ablate & 32u)) each_group(bm, std::false_type{});
+                    wave_sync();
+                    (void)__builtin_amdgcn_readfirstlane(L0[0]);
+                    mark(1);  // bitmap pass
+                    // 2. word ranks into W[w].y, over the touched 64-word blocks only: block b's words
+                    //    are b*64 + lane, a wave scan per block carried across blocks
+                    bmask = wave_or_u32(bm.blk);
+                    for (uint32_t m = bmask; m; m &= m - 1) {
+                        const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
+                        const uint32_t c = __popc(W[w].x);
+                        const uint32_t incl = wave_incl_scan(c, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+                        W[w].y = wcnt + incl - c;
+                        wcnt += readlane_u32(incl, kWave - 1);
+                    }
+                    if (wcnt == 0) return;  // bitmap empty: nothing to clear
                 }
-                if (wcnt == 0) return;  // bitmap empty: nothing to clear
                 mark(2);  // word ranks
                 // narrow u32 slots when the row's sums provably stay below 2^32:
                 // max(A row) * max(B) * len(A row) < 2^32 (each output sums <= len products)
@@ -1084,8 +1138,10 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 } else {
                     run_chunks(std::false_type{}, std::false_type{});
                 }
-                for (uint32_t m = bmask; m; m &= m - 1) W[(uint32_t)__builtin_ctz(m) * kWave + lane].x = 0;
-                wave_sync();
+                if (!stored) {
+                    for (uint32_t m = bmask; m; m &= m - 1) W[(uint32_t)__builtin_ctz(m) * kWave + lane].x = 0;
+                    wave_sync();
+                }
             };
             if (!p.wide) {
                 window(std::true_type{}, 0u);
