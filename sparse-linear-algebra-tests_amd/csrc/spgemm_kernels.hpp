@@ -310,8 +310,14 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
                 mx = max(mx, bm[w]);
                 mn = min(mn, bn[w]);
             }
-            atomicMax(&vmax[kVMaxWord], ((unsigned long long)epoch << 32) | mx);
-            atomicMax(&vmax[kVMinInvWord], ((unsigned long long)epoch << 32) | ~mn);
+            // the words only grow: skip the atomic when the current value already covers ours, so
+            // the blocks of a pattern B (all values equal) do not serialise on one L2 line
+            const unsigned long long wx = ((unsigned long long)epoch << 32) | mx;
+            const unsigned long long wn = ((unsigned long long)epoch << 32) | ~mn;
+            if (__hip_atomic_load(&vmax[kVMaxWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wx)
+                atomicMax(&vmax[kVMaxWord], wx);
+            if (__hip_atomic_load(&vmax[kVMinInvWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wn)
+                atomicMax(&vmax[kVMinInvWord], wn);
         }
     }
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # usage: tools/build_variant.sh NAME "-DFLAG=..." — builds tools/bin/libslat_NAME.so (kernel experiments)
 set -e
+mkdir -p "$(dirname "$0")/bin"
 cd "$(dirname "$0")/../sparse-linear-algebra-tests_amd"
 make -s
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I../include -Icsrc $2 -c csrc/slat_api.hip -o /tmp/slat_$1.o
