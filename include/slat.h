@@ -9,6 +9,11 @@
  *   MagnusMatrix::matmul    src/graph_magnus.rs:224-232      slat_spgemm_csr_sat64
  *   MagnusMatrix::matmul_seq src/graph_magnus.rs:234-242     slat_spgemm_csr_sat64
  *   linalg Csr<u32,f64>::matmul{,_par} linalg/src/csr.rs:308-466  slat_spgemm_csr_f64
+ *   CsrMatrix::add          src/graph_csr.rs:487-542         slat_csr_add
+ *   CsrMatrix::identity     src/graph_csr.rs:68-80           slat_csr_identity
+ *   CsrMatrix::reachability_sum    src/graph_csr.rs:545-559  slat_reachability_sum
+ *   CsrMatrix::power_until_stable  src/graph_csr.rs:562-577  slat_power_until_stable
+ *   CsrMatrix::connected_components src/graph_csr.rs:580-603 slat_connected_components
  *   assert_eq!(self.n, other.n) panics (graph_csr.rs:307,351)  -> SLAT_EDIM
  *
  * Conventions:
@@ -124,6 +129,29 @@ slat_status slat_spgemm_csr_f64(slat_ctx *ctx, const slat_csr_view *A, const sla
  * row-block partition used across GPUs. */
 slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
                                  uint64_t row_end, const slat_csr_view *B, slat_csr *C, uint32_t flags);
+
+/* --- the reference's SpGEMM consumers, device-resident --------------
+ * Square matrices (n_rows == n_cols) for the iterated drivers; host views are staged to the device.
+ * Loop decisions (nnz, pattern equality) are the only host round trips. */
+/* CsrMatrix::add (src/graph_csr.rs:487-542), MagnusMatrix::add (src/graph_magnus.rs:245-300):
+ * per-row sorted union; equal columns combine with the saturating add (u32 / Sat64) or f64 `+`,
+ * a sum of exactly zero is dropped, unmatched entries are copied. Shape mismatch -> SLAT_EDIM. */
+slat_status slat_csr_add(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, slat_csr *C);
+/* CsrMatrix::identity (src/graph_csr.rs:68-80): n x n, values 1. */
+slat_status slat_csr_identity(slat_ctx *ctx, uint64_t n, int32_t dtype, slat_csr *out);
+/* *equal = 1 iff nnz, row_ptr and col_idx agree (the stability test of power_until_stable,
+ * src/graph_csr.rs:567-569). Device-resident views only. */
+slat_status slat_csr_pattern_equal(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B,
+                                   int32_t *equal);
+/* CsrMatrix::reachability_sum (src/graph_csr.rs:545-559): sum = A + A^2 + ... until nnz(sum)
+ * repeats; *k = the last power added. */
+slat_status slat_reachability_sum(slat_ctx *ctx, const slat_csr_view *A, slat_csr *sum, uint64_t *k);
+/* CsrMatrix::power_until_stable (src/graph_csr.rs:562-577): repeated squaring until the pattern
+ * is stable; *k = squarings. */
+slat_status slat_power_until_stable(slat_ctx *ctx, const slat_csr_view *A, slat_csr *out, uint64_t *k);
+/* CsrMatrix::connected_components (src/graph_csr.rs:580-603): closure of A + I, then component ids
+ * numbered by smallest member; `component` = host array of n_rows u64 (usize). */
+slat_status slat_connected_components(slat_ctx *ctx, const slat_csr_view *A, uint64_t *component);
 
 /* --- host-side input generators (the reference's constructors) ------------------------------ */
 /* Host CSR owned by the library (malloc); free with slat_host_csr_free. */

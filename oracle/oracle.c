@@ -657,3 +657,125 @@ uint64_t orc_flops(const orc_csr *a, const orc_csr *b) {
     }
     return f;
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * The reference's SpGEMM consumers, restated over orc_matmul_seq / orc_add.
+ * ------------------------------------------------------------------------------------------- */
+static int orc_clone(const orc_csr *m, orc_csr *out) { return orc_convert(m, m->dtype, out); }
+
+/* CsrMatrix::identity (src/graph_csr.rs:68-80): values 1. */
+int orc_identity(uint64_t n, int dtype, orc_csr *out) {
+    const size_t vs = vsize(dtype);
+    out->n = n;
+    out->nnz = n;
+    out->dtype = dtype;
+    out->row_ptr = (uint64_t *)malloc((n + 1) * 8);
+    out->col = (uint32_t *)malloc(n ? n * 4 : 4);
+    out->val = malloc(n ? n * vs : 8);
+    for (uint64_t i = 0; i <= n; ++i) out->row_ptr[i] = i;
+    for (uint64_t i = 0; i < n; ++i) {
+        out->col[i] = (uint32_t)i;
+        if (dtype == ORC_U32) ((uint32_t *)out->val)[i] = 1;
+        else if (dtype == ORC_SAT64) ((uint64_t *)out->val)[i] = 1;
+        else ((double *)out->val)[i] = 1.0;
+    }
+    return 0;
+}
+
+/* next.nnz() == cur.nnz() && row_ptr == && col_idx == (src/graph_csr.rs:567-569) */
+static int same_pattern(const orc_csr *a, const orc_csr *b) {
+    return a->nnz == b->nnz && a->n == b->n && memcmp(a->row_ptr, b->row_ptr, (a->n + 1) * 8) == 0 &&
+           (a->nnz == 0 || memcmp(a->col, b->col, a->nnz * 4) == 0);
+}
+
+/* CsrMatrix::power_until_stable (src/graph_csr.rs:562-577): repeated squaring until the pattern
+ * of the square equals the pattern of the matrix; *k = squarings done. */
+int orc_power_until_stable(const orc_csr *a, uint64_t *k, orc_csr *out) {
+    orc_csr cur;
+    int rc = orc_clone(a, &cur);
+    if (rc) return rc;
+    *k = 0;
+    for (;;) {
+        orc_csr next;
+        if ((rc = orc_matmul_seq(&cur, &cur, &next))) {
+            orc_csr_free(&cur);
+            return rc;
+        }
+        *k += 1;
+        const int stable = same_pattern(&next, &cur);
+        orc_csr_free(&cur);
+        cur = next;
+        if (stable) break;
+    }
+    *out = cur;
+    return 0;
+}
+
+/* CsrMatrix::reachability_sum (src/graph_csr.rs:545-559): A + A^2 + ... until nnz(sum) repeats;
+ * *k = the last power added. */
+int orc_reachability_sum(const orc_csr *a, uint64_t *k, orc_csr *out) {
+    orc_csr power, sum;
+    int rc;
+    if ((rc = orc_clone(a, &power))) return rc;
+    if ((rc = orc_clone(a, &sum))) {
+        orc_csr_free(&power);
+        return rc;
+    }
+    *k = 1;
+    for (;;) {
+        orc_csr np, ns;
+        if ((rc = orc_matmul_seq(&power, a, &np))) break;
+        orc_csr_free(&power);
+        power = np;
+        *k += 1;
+        if ((rc = orc_add(&sum, &power, &ns))) break;
+        const int done = ns.nnz == sum.nnz;
+        orc_csr_free(&sum);
+        sum = ns;
+        if (done) break;
+    }
+    orc_csr_free(&power);
+    if (rc) {
+        orc_csr_free(&sum);
+        return rc;
+    }
+    *out = sum;
+    return 0;
+}
+
+static int has_entry(const orc_csr *m, uint64_t r, uint32_t c) {
+    uint64_t lo = m->row_ptr[r], hi = m->row_ptr[r + 1];
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (m->col[mid] < c) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < m->row_ptr[r + 1] && m->col[lo] == c;  /* stored entries are non-zero */
+}
+
+/* CsrMatrix::connected_components (src/graph_csr.rs:580-603): closure of A + I by
+ * power_until_stable, then ids in order of each component's smallest node. */
+int orc_connected_components(const orc_csr *a, uint64_t *component) {
+    orc_csr id, with_id, closure;
+    uint64_t k;
+    int rc;
+    if ((rc = orc_identity(a->n, a->dtype, &id))) return rc;
+    rc = orc_add(a, &id, &with_id);
+    orc_csr_free(&id);
+    if (rc) return rc;
+    rc = orc_power_until_stable(&with_id, &k, &closure);
+    orc_csr_free(&with_id);
+    if (rc) return rc;
+    const uint64_t n = a->n;
+    for (uint64_t i = 0; i < n; ++i) component[i] = UINT64_MAX;
+    uint64_t next_id = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (component[i] != UINT64_MAX) continue;
+        const uint64_t cid = next_id++;
+        component[i] = cid;
+        for (uint64_t j = i + 1; j < n; ++j)
+            if (has_entry(&closure, i, (uint32_t)j) && has_entry(&closure, j, (uint32_t)i)) component[j] = cid;
+    }
+    orc_csr_free(&closure);
+    return 0;
+}

@@ -17,6 +17,10 @@
  *                    linalg Csr<u32,f64>::matmul linalg/src/csr.rs:308-356  (f64, left fold)
  *   orc_matmul_par   CsrMatrix::matmul_par       src/graph_csr.rs:350-484   (two-pass, threads)
  *   orc_add          CsrMatrix::add              src/graph_csr.rs:487-542
+ *   orc_identity     CsrMatrix::identity         src/graph_csr.rs:68-80
+ *   orc_reachability_sum      CsrMatrix::reachability_sum      src/graph_csr.rs:545-559
+ *   orc_power_until_stable    CsrMatrix::power_until_stable    src/graph_csr.rs:562-577
+ *   orc_connected_components  CsrMatrix::connected_components  src/graph_csr.rs:580-603
  *
  * Parity pin: see tests/golden/ (nnz sequence that rounds to README.md:41-46, SHA-256 of the
  * arrays computed independently by tests/golden/make_golden.py with numpy+scipy).
@@ -63,6 +67,10 @@ int orc_matmul_seq(const orc_csr *a, const orc_csr *b, orc_csr *out);
 int orc_matmul_par(const orc_csr *a, const orc_csr *b, int nthreads, orc_csr *out);
 int orc_add(const orc_csr *a, const orc_csr *b, orc_csr *out);
 uint64_t orc_flops(const orc_csr *a, const orc_csr *b);
+int orc_identity(uint64_t n, int dtype, orc_csr *out);
+int orc_power_until_stable(const orc_csr *a, uint64_t *k, orc_csr *out);
+int orc_reachability_sum(const orc_csr *a, uint64_t *k, orc_csr *out);
+int orc_connected_components(const orc_csr *a, uint64_t *component);
 
 #ifdef __cplusplus
 }

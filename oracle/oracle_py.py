@@ -62,6 +62,10 @@ def lib():
         L.orc_add.argtypes = [P(_Csr), P(_Csr), P(_Csr)]
         L.orc_flops.argtypes = [P(_Csr), P(_Csr)]
         L.orc_flops.restype = C.c_uint64
+        L.orc_identity.argtypes = [C.c_uint64, C.c_int, P(_Csr)]
+        L.orc_power_until_stable.argtypes = [P(_Csr), P(C.c_uint64), P(_Csr)]
+        L.orc_reachability_sum.argtypes = [P(_Csr), P(C.c_uint64), P(_Csr)]
+        L.orc_connected_components.argtypes = [P(_Csr), C.c_void_p]
         _lib = L
     return _lib
 
@@ -184,8 +188,31 @@ def flops(a: Csr, b: Csr) -> int:
 
 
 def identity(n: int, dtype: int = U32) -> Csr:
-    r = np.arange(n, dtype=np.uint32)
-    return from_coo(n, r, r, np.ones(n), dtype)
+    """CsrMatrix::identity (src/graph_csr.rs:68-80)."""
+    return _new(lib().orc_identity, n, dtype)
+
+
+def power_until_stable(a: Csr):
+    """CsrMatrix::power_until_stable (src/graph_csr.rs:562-577) -> (matrix, squarings)."""
+    k = C.c_uint64()
+    m = _new(lib().orc_power_until_stable, C.byref(a._raw), C.byref(k))
+    return m, int(k.value)
+
+
+def reachability_sum(a: Csr):
+    """CsrMatrix::reachability_sum (src/graph_csr.rs:545-559) -> (sum, last power)."""
+    k = C.c_uint64()
+    m = _new(lib().orc_reachability_sum, C.byref(a._raw), C.byref(k))
+    return m, int(k.value)
+
+
+def connected_components(a: Csr) -> np.ndarray:
+    """CsrMatrix::connected_components (src/graph_csr.rs:580-603) -> component id per node."""
+    out = np.empty(max(a.n, 1), np.uint64)
+    rc = lib().orc_connected_components(C.byref(a._raw), out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"oracle call failed rc={rc}")
+    return out[:a.n]
 
 
 def torus_thinned(side: int, epn: float, rng: Rng) -> Csr:

@@ -18,67 +18,10 @@
 #include <string>
 
 #include "slat.h"
+#include "slat_internal.hpp"
 #include "spgemm_kernels.hpp"
 
 using namespace slat;
-
-struct slat_ctx {
-    int device = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    std::string err;
-    int cu_count = 256;
-    size_t lds_per_block_max = 65536;
-    // workspace (grown on demand)
-    void *ws = nullptr;
-    size_t ws_bytes = 0;
-    unsigned long long *h_shards = nullptr;  // pinned (stats / max-row read-backs)
-    unsigned long long *h_out = nullptr;     // mapped pinned: [0] nnz, [1] max row nnz, [2] rows with zeros
-    unsigned long long *h_out_dev = nullptr; // its device alias (written by k_scan_rows / k_numeric)
-    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word
-    unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
-    uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
-    unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
-    uint64_t status_cap = 0;                 // tiles d_status holds
-    unsigned long long ticket_base = 0;      // tiles handed out so far (the ticket is monotonic)
-    uint32_t scan_epoch = 0;                 // tag of the status / max-row words (22 bits)
-    size_t free_b = 0;                       // cached hipMemGetInfo free bytes
-    uint32_t free_age = 0;
-    hipEvent_t ev[6] = {};
-    slat_stats stats = {};
-};
-
-#define SLAT_HIP(ctx, expr)                                                                        \
-    do {                                                                                           \
-        hipError_t e_ = (expr);                                                                    \
-        if (e_ != hipSuccess) {                                                                    \
-            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                        \
-            return SLAT_EHIP;                                                                      \
-        }                                                                                          \
-    } while (0)
-
-static slat_status fail(slat_ctx *ctx, slat_status s, const std::string &msg) {
-    if (ctx) ctx->err = msg;
-    return s;
-}
-
-static size_t vsize(int32_t dtype) { return dtype == SLAT_U32 ? 4 : 8; }
-
-// C arrays in one stream-ordered pool block (one malloc, one free per matrix):
-// row_ptr | col_idx | values, each 256-byte aligned. alloc = 1 marks the layout for slat_csr_free.
-enum { kAllocSeparate = 0, kAllocJoint = 1 };
-static hipError_t alloc_joint(slat_csr *m, uint64_t nrows, uint64_t cap, size_t vs, hipStream_t s) {
-    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t rp_b = up((nrows + 1) * 8), col_b = up(std::max<uint64_t>(cap, 1) * 4);
-    uint8_t *base = nullptr;
-    const hipError_t e = hipMallocAsync((void **)&base, rp_b + col_b + std::max<uint64_t>(cap, 1) * vs, s);
-    if (e != hipSuccess) return e;
-    m->row_ptr = (uint64_t *)base;
-    m->col_idx = (uint32_t *)(base + rp_b);
-    m->values = base + rp_b + col_b;
-    m->alloc = kAllocJoint;
-    return hipSuccess;
-}
 
 extern "C" {
 
@@ -212,7 +155,7 @@ slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m) {
 }  // extern "C"
 
 // ---------------------------------------------------------------------------------------------
-static slat_status ensure_ws(slat_ctx *ctx, size_t bytes) {
+slat_status slat_ensure_ws(slat_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return SLAT_OK;
     SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->ws) SLAT_HIP(ctx, hipFree(ctx->ws));
@@ -225,7 +168,7 @@ static slat_status ensure_ws(slat_ctx *ctx, size_t bytes) {
     return SLAT_OK;
 }
 
-static slat_status check_view(slat_ctx *ctx, const slat_csr_view *v, const char *name) {
+slat_status slat_check_view(slat_ctx *ctx, const slat_csr_view *v, const char *name) {
     if (!v) return fail(ctx, SLAT_EINVAL, std::string(name) + " is null");
     if (v->dtype < SLAT_U32 || v->dtype > SLAT_F64) return fail(ctx, SLAT_EINVAL, std::string(name) + ": bad dtype");
     if (v->n_rows && !v->row_ptr) return fail(ctx, SLAT_EINVAL, std::string(name) + ": null row_ptr");
@@ -236,7 +179,7 @@ static slat_status check_view(slat_ctx *ctx, const slat_csr_view *v, const char 
 
 extern "C" slat_status slat_csr_create(slat_ctx *ctx, const slat_csr_view *src, slat_csr *out) {
     if (!ctx || !out) return SLAT_EINVAL;
-    slat_status st = check_view(ctx, src, "src");
+    slat_status st = slat_check_view(ctx, src, "src");
     if (st) return st;
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
     std::memset(out, 0, sizeof *out);
@@ -275,7 +218,7 @@ extern "C" slat_status slat_csr_create(slat_ctx *ctx, const slat_csr_view *src, 
 extern "C" slat_status slat_csr_to_host(slat_ctx *ctx, const slat_csr_view *src, uint64_t *row_ptr, uint32_t *col,
                                         void *vals) {
     if (!ctx) return SLAT_EINVAL;
-    slat_status st = check_view(ctx, src, "src");
+    slat_status st = slat_check_view(ctx, src, "src");
     if (st) return st;
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
     const hipMemcpyKind kind = src->residency == SLAT_HOST ? hipMemcpyHostToHost : hipMemcpyDeviceToHost;
@@ -296,7 +239,7 @@ extern "C" slat_status slat_csr_max_row_nnz(slat_ctx *ctx, const slat_csr_view *
         *out = mr;
         return SLAT_OK;
     }
-    slat_status st = ensure_ws(ctx, 4096);
+    slat_status st = slat_ensure_ws(ctx, 4096);
     if (st) return st;
     unsigned long long *shards = (unsigned long long *)ctx->ws;
     SLAT_HIP(ctx, hipMemsetAsync(shards, 0, sizeof(unsigned long long) * kShards * kShardStride, ctx->stream));
@@ -383,7 +326,7 @@ static hipError_t launch_compact(dim3 grid, hipStream_t s, const uint64_t *orp, 
 
 // row_ptr[0..n] of a count vector: k_scan_rows (one kernel); the total and the max count land in
 // ctx->h_out[0], [1] once the stream reaches that point
-static slat_status launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s) {
+slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s) {
     const uint64_t tiles = std::max<uint64_t>((n + kScanTile - 1) / kScanTile, 1);
     if (tiles > ctx->status_cap) {
         if (ctx->d_status) SLAT_HIP(ctx, hipFreeAsync(ctx->d_status, s));
@@ -424,7 +367,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                                             uint64_t row_end, const slat_csr_view *B, slat_csr *C, uint32_t flags) {
     if (!ctx || !C) return SLAT_EINVAL;
     slat_status st;
-    if ((st = check_view(ctx, A, "A")) || (st = check_view(ctx, B, "B"))) return st;
+    if ((st = slat_check_view(ctx, A, "A")) || (st = slat_check_view(ctx, B, "B"))) return st;
     if (A->dtype != B->dtype) return fail(ctx, SLAT_EINVAL, "A and B value types differ");
     if (A->n_cols != B->n_rows) return fail(ctx, SLAT_EDIM, "A.n_cols != B.n_rows");
     if (B->n_cols > 0xFFFFFFFFull - (1ull << 17))  // column ids are u32; the top 2^17 values stay free
@@ -537,7 +480,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
-    if ((st = ensure_ws(ctx, o_smask + smask_b))) return st;
+    if ((st = slat_ensure_ws(ctx, o_smask + smask_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (ell) {
         a.ell_wq = (uint32_t)wq;
@@ -611,7 +554,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     launch_symbolic(idx32, ell, sym_grid, sym_lds, s, asym);
     SLAT_HIP(ctx, hipGetLastError());
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
-    if ((st = launch_scan(ctx, a.counts, n, C->row_ptr, s))) return st;
+    if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s))) return st;
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
 
     if (exact) {
@@ -671,7 +614,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         // exact zeros were dropped: rebuild row_ptr from the per-row actual counts and move rows
         uint64_t *nrp = nullptr;
         SLAT_HIP(ctx, hipMallocAsync((void **)&nrp, (n + 1) * 8, s));
-        if ((st = launch_scan(ctx, a.counts, n, nrp, s))) return st;
+        if ((st = slat_launch_scan(ctx, a.counts, n, nrp, s))) return st;
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         const uint64_t total = ctx->h_out[0];
         maxrow = ctx->h_out[1];

@@ -1,0 +1,76 @@
+// slat_internal.hpp — the context and host helpers shared by the library's translation units
+// (slat_api.hip: SpGEMM; slat_graph.hip: the reference's SpGEMM consumers). Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+
+#include "slat.h"
+
+struct slat_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int cu_count = 256;
+    size_t lds_per_block_max = 65536;
+    // workspace (grown on demand)
+    void *ws = nullptr;
+    size_t ws_bytes = 0;
+    unsigned long long *h_shards = nullptr;  // pinned (stats / max-row read-backs)
+    unsigned long long *h_out = nullptr;     // mapped pinned: [0] nnz, [1] max row nnz, [2] rows with zeros
+    unsigned long long *h_out_dev = nullptr; // its device alias (written by k_scan_rows / k_numeric)
+    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word
+    unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
+    uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
+    unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
+    uint64_t status_cap = 0;                 // tiles d_status holds
+    unsigned long long ticket_base = 0;      // tiles handed out so far (the ticket is monotonic)
+    uint32_t scan_epoch = 0;                 // tag of the status / max-row words (22 bits)
+    size_t free_b = 0;                       // cached hipMemGetInfo free bytes
+    uint32_t free_age = 0;
+    hipEvent_t ev[6] = {};
+    slat_stats stats = {};
+};
+
+#define SLAT_HIP(ctx, expr)                                                                        \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                        \
+            return SLAT_EHIP;                                                                      \
+        }                                                                                          \
+    } while (0)
+
+static inline slat_status fail(slat_ctx *ctx, slat_status s, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return s;
+}
+
+static inline size_t vsize(int32_t dtype) { return dtype == SLAT_U32 ? 4 : 8; }
+
+// C arrays in one stream-ordered pool block (one malloc, one free per matrix):
+// row_ptr | col_idx | values, each 256-byte aligned. alloc = 1 marks the layout for slat_csr_free.
+enum { kAllocSeparate = 0, kAllocJoint = 1 };
+static inline hipError_t alloc_joint(slat_csr *m, uint64_t nrows, uint64_t cap, size_t vs, hipStream_t s) {
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t rp_b = up((nrows + 1) * 8), col_b = up(std::max<uint64_t>(cap, 1) * 4);
+    uint8_t *base = nullptr;
+    const hipError_t e = hipMallocAsync((void **)&base, rp_b + col_b + std::max<uint64_t>(cap, 1) * vs, s);
+    if (e != hipSuccess) return e;
+    m->row_ptr = (uint64_t *)base;
+    m->col_idx = (uint32_t *)(base + rp_b);
+    m->values = base + rp_b + col_b;
+    m->alloc = kAllocJoint;
+    return hipSuccess;
+}
+
+// workspace of at least `bytes` in ctx->ws (grown with a stream sync; contents not kept)
+slat_status slat_ensure_ws(slat_ctx *ctx, size_t bytes);
+// structural checks of a view (dtype, null arrays, u32 ids)
+slat_status slat_check_view(slat_ctx *ctx, const slat_csr_view *v, const char *name);
+// rp[0..n] = exclusive prefix of counts[0..n) (rp[n] = total) by k_scan_rows on stream s; the total
+// and the max count land in ctx->h_out[0], [1] once the stream reaches that point
+slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s);

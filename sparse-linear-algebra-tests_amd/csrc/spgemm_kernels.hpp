@@ -1193,7 +1193,7 @@ __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long l
     return v;
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_t *counts, uint64_t n, uint64_t *rp,
+static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_t *counts, uint64_t n, uint64_t *rp,
                                                             unsigned long long *status, unsigned long long *ticket,
                                                             unsigned long long ticket_base, uint32_t epoch,
                                                             unsigned long long *maxw, unsigned long long *host_out) {
@@ -1302,7 +1302,7 @@ __global__ __launch_bounds__(kBlock) void k_compact(const uint64_t *old_rp, cons
 }
 
 // max over rows of row_ptr[i+1] - row_ptr[i]
-__global__ __launch_bounds__(kBlock) void k_max_row(const uint64_t *rp, uint64_t nrows, unsigned long long *shards) {
+static __global__ __launch_bounds__(kBlock) void k_max_row(const uint64_t *rp, uint64_t nrows, unsigned long long *shards) {
     __shared__ unsigned long long red[kBlock];
     unsigned long long m = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nrows; i += (uint64_t)gridDim.x * kBlock)

@@ -22,6 +22,8 @@ EXPORTS = [
     "slat_csr_view_of", "slat_csr_max_row_nnz", "slat_spgemm", "slat_spgemm_csr_u32", "slat_spgemm_csr_sat64",
     "slat_spgemm_csr_f64", "slat_spgemm_rowblock", "slat_rng_seed", "slat_rng_next_u64", "slat_rng_next_f64",
     "slat_host_from_coo", "slat_host_lattice", "slat_host_thin", "slat_host_rmat", "slat_host_csr_free",
+    "slat_csr_add", "slat_csr_identity", "slat_csr_pattern_equal", "slat_reachability_sum",
+    "slat_power_until_stable", "slat_connected_components",
 ]
 
 
@@ -108,6 +110,12 @@ def lib():
         "slat_host_thin": ([P(HostCsr), P(RngState), C.c_double, P(HostCsr)], C.c_int),
         "slat_host_rmat": ([u32, u64, C.c_double, C.c_double, C.c_double, C.c_char_p, P(HostCsr)], C.c_int),
         "slat_host_csr_free": ([P(HostCsr)], None),
+        "slat_csr_add": ([vp, P(CsrView), P(CsrView), P(CsrOwned)], C.c_int),
+        "slat_csr_identity": ([vp, u64, i32, P(CsrOwned)], C.c_int),
+        "slat_csr_pattern_equal": ([vp, P(CsrView), P(CsrView), P(i32)], C.c_int),
+        "slat_reachability_sum": ([vp, P(CsrView), P(CsrOwned), P(u64)], C.c_int),
+        "slat_power_until_stable": ([vp, P(CsrView), P(CsrOwned), P(u64)], C.c_int),
+        "slat_connected_components": ([vp, P(CsrView), vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

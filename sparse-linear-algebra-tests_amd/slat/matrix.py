@@ -213,9 +213,12 @@ class DeviceCsr:
         return cls.from_host(HostCsr(n, np.zeros(n + 1, np.uint64), [], [], cls.DTYPE))
 
     @classmethod
-    def identity(cls, n: int):
-        r = np.arange(n, dtype=np.uint64)
-        return cls.from_host(HostCsr(n, np.arange(n + 1, dtype=np.uint64), r, np.ones(n), cls.DTYPE))
+    def identity(cls, n: int, ctx: Context | None = None):
+        """CsrMatrix::identity (src/graph_csr.rs:68-80), built on the device."""
+        ctx = ctx or default_context()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_identity(ctx.ptr, n, cls.DTYPE, C.byref(out)), ctx.ptr)
+        return cls(out, ctx)
 
     @classmethod
     def from_coo(cls, n: int, triplets: Iterable):
@@ -314,6 +317,49 @@ class DeviceCsr:
         a, b = self.view(), other.view()
         out = L.CsrOwned()
         L.check(L.lib().slat_spgemm(self._ctx.ptr, C.byref(a), C.byref(b), C.byref(out), flags), self._ctx.ptr)
+        return type(self)(out, self._ctx)
+
+    # -- the reference's SpGEMM consumers, device-resident --------------
+    def add(self, other: "DeviceCsr"):
+        """CsrMatrix::add (src/graph_csr.rs:487-542) / MagnusMatrix::add (src/graph_magnus.rs:245-300)."""
+        if type(other) is not type(self):
+            raise TypeError("operands must have the same matrix type")
+        a, b = self.view(), other.view()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_add(self._ctx.ptr, C.byref(a), C.byref(b), C.byref(out)), self._ctx.ptr)
+        return type(self)(out, self._ctx)
+
+    def same_pattern(self, other: "DeviceCsr") -> bool:
+        """nnz, row_ptr and col_idx equal (the test in power_until_stable, src/graph_csr.rs:567-569)."""
+        a, b = self.view(), other.view()
+        eq = C.c_int32()
+        L.check(L.lib().slat_csr_pattern_equal(self._ctx.ptr, C.byref(a), C.byref(b), C.byref(eq)), self._ctx.ptr)
+        return bool(eq.value)
+
+    def reachability_sum(self):
+        """CsrMatrix::reachability_sum (src/graph_csr.rs:545-559) -> (sum, k)."""
+        a, out, k = self.view(), L.CsrOwned(), C.c_uint64()
+        L.check(L.lib().slat_reachability_sum(self._ctx.ptr, C.byref(a), C.byref(out), C.byref(k)), self._ctx.ptr)
+        return type(self)(out, self._ctx), int(k.value)
+
+    def power_until_stable(self):
+        """CsrMatrix::power_until_stable (src/graph_csr.rs:562-577) -> (matrix, k)."""
+        a, out, k = self.view(), L.CsrOwned(), C.c_uint64()
+        L.check(L.lib().slat_power_until_stable(self._ctx.ptr, C.byref(a), C.byref(out), C.byref(k)), self._ctx.ptr)
+        return type(self)(out, self._ctx), int(k.value)
+
+    def connected_components(self) -> list:
+        """CsrMatrix::connected_components (src/graph_csr.rs:580-603) -> Vec<usize> as a list."""
+        comp = np.zeros(max(self.n, 1), np.uint64)
+        a = self.view()
+        L.check(L.lib().slat_connected_components(self._ctx.ptr, C.byref(a), comp.ctypes.data), self._ctx.ptr)
+        return comp[:self.n].tolist()
+
+    def clone(self):
+        """`Clone` of the owned matrix: a device-to-device copy."""
+        v = self.view()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_create(self._ctx.ptr, C.byref(v), C.byref(out)), self._ctx.ptr)
         return type(self)(out, self._ctx)
 
     def matmul_rowblock(self, row_begin: int, row_end: int, other: "DeviceCsr", flags: int = 0):
