@@ -260,6 +260,30 @@ extern "C" slat_status slat_csr_max_row_nnz(slat_ctx *ctx, const slat_csr_view *
 // ---------------------------------------------------------------------------------------------
 template <typename Sem>
 static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
+    // wide launches: the hash category (a.hash == 1) and the window category (a.hash == 2) are
+    // instances of their own, so neither path's registers burden the other
+    if (a.hash == 1) {
+        if (idx32 && ell)
+            hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true, 1>), grid, dim3(kBlock), lds, s, a);
+        else if (idx32)
+            hipLaunchKernelGGL((k_numeric<Sem, uint32_t, false, 1>), grid, dim3(kBlock), lds, s, a);
+        else if (ell)
+            hipLaunchKernelGGL((k_numeric<Sem, uint64_t, true, 1>), grid, dim3(kBlock), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_numeric<Sem, uint64_t, false, 1>), grid, dim3(kBlock), lds, s, a);
+        return hipGetLastError();
+    }
+    if (a.hash == 2) {
+        if (idx32 && ell)
+            hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true, 2>), grid, dim3(kBlock), lds, s, a);
+        else if (idx32)
+            hipLaunchKernelGGL((k_numeric<Sem, uint32_t, false, 2>), grid, dim3(kBlock), lds, s, a);
+        else if (ell)
+            hipLaunchKernelGGL((k_numeric<Sem, uint64_t, true, 2>), grid, dim3(kBlock), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_numeric<Sem, uint64_t, false, 2>), grid, dim3(kBlock), lds, s, a);
+        return hipGetLastError();
+    }
     if (idx32 && ell)
         hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true>), grid, dim3(kBlock), lds, s, a);
     else if (idx32)
@@ -274,22 +298,24 @@ static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hi
 // resident blocks per CU of the numeric kernel instance (its grid is sized to that: the product
 // record in the workspace is indexed by resident wave)
 template <typename Sem>
-static int numeric_blocks_per_cu(bool idx32, bool ell, size_t lds) {
+static int numeric_blocks_per_cu(bool idx32, bool ell, int mode, size_t lds) {
     // cached per (instance, LDS size): the query costs microseconds of host time per call
-    static thread_local int cache_nb[4] = {0, 0, 0, 0};
-    static thread_local size_t cache_lds[4] = {0, 0, 0, 0};
-    const int ci = (idx32 ? 1 : 0) | (ell ? 2 : 0);
+    static thread_local int cache_nb[12] = {};
+    static thread_local size_t cache_lds[12] = {};
+    const int ci = (idx32 ? 1 : 0) | (ell ? 2 : 0) | (mode << 2);
     if (cache_lds[ci] == lds && cache_nb[ci] > 0) return cache_nb[ci];
     int nb = 0;
     hipError_t e;
-    if (idx32 && ell)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint32_t, true>, kBlock, lds);
-    else if (idx32)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint32_t, false>, kBlock, lds);
-    else if (ell)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint64_t, true>, kBlock, lds);
+    auto occ = [&](auto kern) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kBlock, lds); };
+    if (mode == 1)
+        e = idx32 ? (ell ? occ(k_numeric<Sem, uint32_t, true, 1>) : occ(k_numeric<Sem, uint32_t, false, 1>))
+                  : (ell ? occ(k_numeric<Sem, uint64_t, true, 1>) : occ(k_numeric<Sem, uint64_t, false, 1>));
+    else if (mode == 2)
+        e = idx32 ? (ell ? occ(k_numeric<Sem, uint32_t, true, 2>) : occ(k_numeric<Sem, uint32_t, false, 2>))
+                  : (ell ? occ(k_numeric<Sem, uint64_t, true, 2>) : occ(k_numeric<Sem, uint64_t, false, 2>));
     else
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_numeric<Sem, uint64_t, false>, kBlock, lds);
+        e = idx32 ? (ell ? occ(k_numeric<Sem, uint32_t, true>) : occ(k_numeric<Sem, uint32_t, false>))
+                  : (ell ? occ(k_numeric<Sem, uint64_t, true>) : occ(k_numeric<Sem, uint64_t, false>));
     nb = (e == hipSuccess && nb > 0) ? nb : 1;
     cache_lds[ci] = lds;
     cache_nb[ci] = nb;
@@ -297,6 +323,17 @@ static int numeric_blocks_per_cu(bool idx32, bool ell, size_t lds) {
 }
 
 static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
+    if (a.hash == 1 || a.hash == 2) {
+        auto go = [&](auto kern) { kern<<<grid, dim3(kBlock), lds, s>>>(a); };
+        if (a.hash == 1) {
+            if (idx32) ell ? go(k_symbolic<uint32_t, true, 1>) : go(k_symbolic<uint32_t, false, 1>);
+            else ell ? go(k_symbolic<uint64_t, true, 1>) : go(k_symbolic<uint64_t, false, 1>);
+        } else {
+            if (idx32) ell ? go(k_symbolic<uint32_t, true, 2>) : go(k_symbolic<uint32_t, false, 2>);
+            else ell ? go(k_symbolic<uint64_t, true, 2>) : go(k_symbolic<uint64_t, false, 2>);
+        }
+        return;
+    }
     if (idx32 && ell)
         hipLaunchKernelGGL((k_symbolic<uint32_t, true>), grid, dim3(kBlock), lds, s, a);
     else if (idx32)
@@ -439,6 +476,17 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     pick_window(ncols, kWave, 1984, asym.ww, asym.wide);
     pick_window(ncols, kWave, 1984, a.ww, a.wide);
     a.area = 896 * 6;  // rank slots per wave: 896 narrow (u32 + u16) slots; 3 blocks/CU at the 30^3 window
+    // Wide launches (columns beyond one window): short rows take the per-wave LDS hash table
+    // (MAGNUS's small-row category); the rest keep row-span windows, made small so the shared
+    // region stays small: symbolic 1024 words (the hash keys' size), numeric 256 words.
+    // Wide launches (columns beyond one window) split the rows by MAGNUS-style category into two
+    // launches per pass: short rows in a per-wave LDS hash table (mode 1), the rest by row-span
+    // windows (mode 2; numeric windows of 1024 words keep two blocks per CU).
+    const bool hash = asym.wide && !std::getenv("SLAT_NO_HASH");
+    if (hash) {
+        a.ww = std::min<uint32_t>(a.ww, 1024);
+        a.b_maxrow = asym.b_maxrow = (uint32_t)std::min<uint64_t>(maxrow_b, 0xFFFFFFFFull);
+    }
     // padded ELL copy of B when its rows are short (bounded blow-up)
     const uint64_t wq = (maxrow_b + 3) / 4;
     const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
@@ -452,14 +500,21 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (const char *e_ = std::getenv("SLAT_CAP")) a.area = 6 * std::max(64, std::atoi(e_));  // tuning knob
     a.area = (a.area + 15) & ~15u;
     const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.area).bytes;
+    const size_t hash_lds = (size_t)wpb * (dt == SLAT_U32     ? hash_bytes<SemU32>()
+                                           : dt == SLAT_SAT64 ? hash_bytes<SemSat64>()
+                                                              : hash_bytes<SemF64>());
     if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
-    const size_t sym_lds = (size_t)wpb * asym.ww * 4;
+    const size_t sym_lds = (size_t)wpb * asym.ww * 4, sym_hash_lds = (size_t)wpb * kSymHashT * 4;
     const uint64_t row_blocks = (n + wpb - 1) / wpb;
     const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * 16)));
-    const int nbpc = dt == SLAT_U32     ? numeric_blocks_per_cu<SemU32>(idx32, ell, num_lds)
-                     : dt == SLAT_SAT64 ? numeric_blocks_per_cu<SemSat64>(idx32, ell, num_lds)
-                                        : numeric_blocks_per_cu<SemF64>(idx32, ell, num_lds);
-    const dim3 grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc)));
+    auto num_grid = [&](int mode, size_t lds) {
+        const int nbpc = dt == SLAT_U32     ? numeric_blocks_per_cu<SemU32>(idx32, ell, mode, lds)
+                         : dt == SLAT_SAT64 ? numeric_blocks_per_cu<SemSat64>(idx32, ell, mode, lds)
+                                            : numeric_blocks_per_cu<SemF64>(idx32, ell, mode, lds);
+        return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc)));
+    };
+    const dim3 grid = num_grid(hash ? 2 : 0, num_lds);
+    const dim3 hash_grid = hash ? num_grid(1, hash_lds) : dim3(1);
     const bool timing = flags & SLAT_FLAG_TIMING;
 
     // workspace: counts [n] | ablation counts [n] | shards | scan temp | ELL cols | ELL vals | ELL groups
@@ -551,7 +606,16 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
     }
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
-    launch_symbolic(idx32, ell, sym_grid, sym_lds, s, asym);
+    if (hash) {
+        Args h1 = asym, h2 = asym;
+        h1.hash = 1;
+        h2.hash = 2;
+        launch_symbolic(idx32, ell, sym_grid, sym_hash_lds, s, h1);
+        SLAT_HIP(ctx, hipGetLastError());
+        launch_symbolic(idx32, ell, sym_grid, sym_lds, s, h2);
+    } else {
+        launch_symbolic(idx32, ell, sym_grid, sym_lds, s, asym);
+    }
     SLAT_HIP(ctx, hipGetLastError());
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
     if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s))) return st;
@@ -585,6 +649,16 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
         SLAT_HIP(ctx, launch_num(abl));
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
+    }
+    if (hash) {
+        Args h1 = a;
+        h1.hash = 1;
+        a.hash = 2;
+        hipError_t he;
+        if (dt == SLAT_U32) he = launch_numeric<SemU32>(idx32, ell, hash_grid, hash_lds, s, h1);
+        else if (dt == SLAT_SAT64) he = launch_numeric<SemSat64>(idx32, ell, hash_grid, hash_lds, s, h1);
+        else he = launch_numeric<SemF64>(idx32, ell, hash_grid, hash_lds, s, h1);
+        SLAT_HIP(ctx, he);
     }
     SLAT_HIP(ctx, launch_num(a));
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));

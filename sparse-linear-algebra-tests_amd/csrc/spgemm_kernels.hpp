@@ -45,6 +45,7 @@ constexpr int kShards = 64;      // sharded status words (avoid one hot atomic a
 constexpr uint32_t kSent = 0xFFFFFFFFu;  // ELL padding (column ids are < n_cols <= 2^32 - 1)
 // words of the B-value summary block (context memory, epoch-tagged): max B value, ~min B value
 constexpr int kVMaxWord = 0, kVMinInvWord = 3;
+constexpr int kRegQ = 4;  // A entries per lane kept in registers across the numeric passes
 constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2] rows with zeros, [3] flops
 
 #ifndef SLAT_PHASES
@@ -92,6 +93,10 @@ struct Args {
     uint32_t *sbm;
     uint32_t *smask;
     uint32_t nblk;
+    // MAGNUS-style short-row category (wide launches): rows whose outputs fit a per-wave LDS hash
+    // table accumulate there and emit by rank-by-count instead of bitmap windows (0 = off)
+    uint32_t hash;
+    uint32_t b_maxrow;  // max row length of B (the symbolic pass's product bound: len(A row) * b_maxrow)
     unsigned long long *host_out;  // mapped pinned host words: [0] nnz, [1] max row nnz, [2] rows with zeros
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
@@ -453,6 +458,122 @@ __device__ __forceinline__ bool win_off(uint32_t c, uint32_t wlo, uint32_t WIN, 
 
 
 // ------------------------------------------------------------------------------------------------
+// Short rows of wide launches (MAGNUS's accumulation of rows whose outputs fit a small table): an
+// LDS hash table per wave, keys = column ids (kSent = empty, never a column), linear probing.
+// Symbolic counts the inserted keys; numeric accumulates values in the slots, then every lane
+// ranks the keys it holds by counting the smaller ones among all of the row's keys (broadcast
+// reads of a staged key list) and writes (col, value) at out + rank: sorted output, no sort pass.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kHashT = 512;      // numeric slots per wave (rows with <= kHashT / 2 outputs)
+constexpr uint32_t kSymHashT = 1024;  // symbolic keys per wave (rows with <= 0.7 * kSymHashT products)
+constexpr uint32_t kHashHeld = kHashT / kWave;
+
+__device__ __forceinline__ uint32_t hash_slot(uint32_t c, uint32_t logt) { return (c * 0x9E3779B1u) >> (32 - logt); }
+
+// slots of N columns at once (kSent = no column): every probe round issues all pending CAS
+// before it looks at any result, so the LDS latency is paid once per round, not once per column.
+// fresh[i]: this call inserted column i.
+template <int N>
+__device__ __forceinline__ void hash_batch(uint32_t *keys, uint32_t logt, const uint32_t (&c)[N], uint32_t (&sl)[N],
+                                           bool (&fresh)[N]) {
+    const uint32_t mask = (1u << logt) - 1;
+    uint32_t pend = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        sl[i] = hash_slot(c[i], logt);
+        fresh[i] = false;
+        if (c[i] != kSent) pend |= 1u << i;
+    }
+    while (__builtin_amdgcn_readfirstlane(__ballot(pend != 0) != 0)) {
+        uint32_t prev[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (pend & (1u << i)) prev[i] = atomicCAS(&keys[sl[i]], kSent, c[i]);
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if (pend & (1u << i)) {
+                if (prev[i] == kSent || prev[i] == c[i]) {
+                    fresh[i] = prev[i] == kSent;
+                    pend &= ~(1u << i);
+                } else {
+                    sl[i] = (sl[i] + 1) & mask;
+                }
+            }
+    }
+}
+
+// symbolic: distinct columns of the row = keys this wave inserted
+struct HashCount {
+    uint32_t *keys;
+    uint32_t cnt = 0, nprod = 0;
+    template <int Q>
+    __device__ __forceinline__ void run(const uint4 *c) {
+        uint32_t cc[4 * Q], sl[4 * Q];
+        bool fresh[4 * Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            cc[4 * q] = c[q].x;
+            cc[4 * q + 1] = c[q].y;
+            cc[4 * q + 2] = c[q].z;
+            cc[4 * q + 3] = c[q].w;
+        }
+        hash_batch<4 * Q>(keys, 10, cc, sl, fresh);  // kSymHashT = 2^10
+#pragma unroll
+        for (int i = 0; i < 4 * Q; ++i) {
+            cnt += fresh[i] ? 1u : 0u;
+            nprod += cc[i] != kSent ? 1u : 0u;
+        }
+    }
+    __device__ __forceinline__ void operator()(uint4 c, const Quad<uint32_t> &) { run<1>(&c); }
+    // one quad (4 columns) per probe batch: wider batches cost more registers than they save
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<uint32_t> *) {
+        sfor<kRegQ>([&](auto Q) { run<1>(c + Q); });
+    }
+};
+
+// numeric: products into the slots of their columns (Sem::acc: atomics for the integer
+// semirings, a plain add for f64, whose ordered walk never has two lanes on one column)
+template <typename Sem>
+struct HashAcc {
+    using S = typename Sem::S;
+    uint32_t *keys;
+    typename Sem::V *vals;
+    template <int Q>
+    __device__ __forceinline__ void run(const uint4 *c, const Quad<S> *pr) {
+        uint32_t cc[4 * Q], sl[4 * Q];
+        bool fresh[4 * Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            cc[4 * q] = c[q].x;
+            cc[4 * q + 1] = c[q].y;
+            cc[4 * q + 2] = c[q].z;
+            cc[4 * q + 3] = c[q].w;
+        }
+        hash_batch<4 * Q>(keys, 9, cc, sl, fresh);  // kHashT = 2^9
+#pragma unroll
+        for (int i = 0; i < 4 * Q; ++i)
+            if (cc[i] != kSent) Sem::acc(vals, sl[i], pr[i / 4].v[i % 4]);
+    }
+    __device__ __forceinline__ void put(uint32_t c, S pr) {
+        uint32_t cc[1] = {c}, sl[1];
+        bool fresh[1];
+        hash_batch<1>(keys, 9, cc, sl, fresh);
+        if (c != kSent) Sem::acc(vals, sl[0], pr);
+    }
+    __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) { run<1>(&c, &pr); }
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
+        sfor<kRegQ>([&](auto Q) { run<1>(c + Q, pr + Q); });
+    }
+};
+
+// Per-wave LDS of the numeric hash path: keys u32[kHashT] | vals V[kHashT * kSlots] | stage
+// u32[kHashT / 2 + 4] (the row's keys, compacted, padded with kSent for 16-byte reads)
+template <typename Sem>
+__host__ __device__ constexpr uint32_t hash_bytes() {
+    return kHashT * 4 + kHashT * (uint32_t)sizeof(typename Sem::V) * Sem::kSlots + (kHashT / 2 + 4) * 4;
+}
+
+// ------------------------------------------------------------------------------------------------
 // numeric: one wavefront per row
 // ------------------------------------------------------------------------------------------------
 struct NumLayout {
@@ -485,7 +606,6 @@ __device__ __forceinline__ uint32_t rank_in(uint2 w, uint32_t off, uint32_t r0, 
     return rk < nch ? rk : kSent;
 }
 
-constexpr int kRegQ = 4;  // A entries per lane kept in registers across the numeric passes
 
 template <typename S>
 __device__ __forceinline__ S permute_val(int dst, S v) {
@@ -742,10 +862,36 @@ struct RowWalker {
 
 __device__ __forceinline__ void pin_u64(unsigned long long v) { pin(v); }
 
+// log2 of the chunk width of SpanPass: 32 chunks cover every column
+__device__ __forceinline__ uint32_t chunk_shift(uint64_t ncols) {
+    uint32_t b = 0;
+    while (b < 58 && (ncols - 1) >> (b + 5)) ++b;
+    return max(b, 5u);
+}
+
+// the windows [wlo, wlo + WIN) of a row spanning [lo, hi]: each next window starts at the first
+// touched chunk at or after the previous window's end
+template <typename F>
+__device__ __forceinline__ void for_windows(uint64_t lo, uint64_t hi, uint32_t WIN, uint32_t cm, uint32_t csh, F &&win) {
+    uint64_t wlo = lo & ~31ull;
+    while (wlo <= hi) {
+        win((uint32_t)wlo);
+        const uint64_t e = wlo + WIN;
+        if (e > hi) break;
+        const uint64_t ce = e >> csh;
+        const uint32_t rest = ce >= 32 ? 0u : (cm >> ce);
+        if (!rest) break;
+        wlo = (rest & 1u) ? e : (ce + (uint64_t)__builtin_ctz(rest)) << csh;
+    }
+}
+
 // numeric pass 1: column span of the row (rows wider than one window)
-template <typename S>
+// plus the mask of touched column chunks (32 chunks of 2^csh columns), so the windows skip the
+// empty stretches of a row whose columns wrap around (a torus row near the boundary)
+template <typename S, bool CHUNKS = false>
 struct SpanPass {
-    uint32_t l = 0xFFFFFFFFu, h = 0;
+    uint32_t csh;
+    uint32_t l = 0xFFFFFFFFu, h = 0, cm = 0;
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &) {
         const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
@@ -753,6 +899,7 @@ struct SpanPass {
             if (cc[e] != kSent) {
                 l = min(l, cc[e]);
                 h = max(h, cc[e]);
+                if constexpr (CHUNKS) cm |= 1u << ((cc[e] >> csh) & 31);
             }
     }
     __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
@@ -838,7 +985,9 @@ struct AccPass {
         if constexpr (SLAT_PHASES) pc->mark(11);  // atomics issued
     }
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) { run<1>(&c, &pr); }
-    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) { run<kRegQ>(c, pr); }
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
+        sfor<kRegQ>([&](auto Q) { run<1>(c + Q, pr + Q); });
+    }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -859,13 +1008,22 @@ struct SymPass {
     }
 };
 
-template <typename I, bool ELL>
+// MODE 0: every row by bitmap windows. Wide launches split the rows in two launches by the
+// MAGNUS-style category (a uniform test on the row: len(A row) * max row of B <= 0.7 kSymHashT):
+// MODE 1 counts the short rows in the LDS hash table and skips the rest, MODE 2 the converse.
+__host__ __device__ constexpr bool sym_short_row(uint64_t len, uint32_t b_maxrow) {
+    return len * b_maxrow <= kSymHashT * 7 / 10;
+}
+
+template <typename I, bool ELL, int MODE = 0>
 __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     constexpr int kWpb = kBlock / kWave;
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
-    uint32_t *L0 = smem + (size_t)wv * p.ww;
+    // per-wave words: the window bitmap, or (MODE 1) the hash keys
+    const uint32_t region_w = MODE == 1 ? kSymHashT : p.ww;
+    uint32_t *L0 = smem + (size_t)wv * region_w;
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) p.c_rp[0] = 0;
         if (threadIdx.x < kShards) {  // fields read by k_numeric; [3] (flops) is zeroed by the host
@@ -873,21 +1031,40 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
             p.shards[threadIdx.x * kShardStride + 2] = 0;
         }
     }
-    for (uint32_t w = lane; w < p.ww; w += kWave) L0[w] = 0;
+    for (uint32_t w = lane; w < region_w; w += kWave) L0[w] = MODE == 1 ? kSent : 0u;
     wave_sync();
     const uint32_t WIN = p.ww * 32;
     unsigned long long flops = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     for (uint64_t row = (uint64_t)blockIdx.x * kWpb + wv; row < p.nrows; row += stride) {
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
+        if constexpr (MODE != 0) {
+            if (sym_short_row((uint64_t)(a1 - a0), p.b_maxrow) != (MODE == 1)) continue;  // the other launch's row
+        }
         uint64_t cnt = 0;
-        if (a1 > a0) {
+        if constexpr (MODE == 1) {
+            if (a1 > a0) {
+                // short row: distinct columns = keys inserted into the wave's hash table
+                RowWalker<SemNone, I, ELL, false> rw(p, a0, a1);
+                HashCount hc{L0};
+                rw.template each_group<false>(hc);
+                wave_sync();
+                cnt = wave_sum_u32(hc.cnt);
+                if (p.stats) flops += wave_sum_u32(hc.nprod);
+                uint4 *k4 = (uint4 *)L0;
+                for (uint32_t w = lane; w < kSymHashT / 4; w += kWave) k4[w] = make_uint4(kSent, kSent, kSent, kSent);
+                wave_sync();
+            }
+        } else if (a1 > a0) {
             RowWalker<SemNone, I, ELL, false> rw(p, a0, a1);
             uint64_t lo = 0, hi = p.ncols - 1;
+            uint32_t cmask = 0xFFFFFFFFu;  // touched column chunks (MODE 2 only; else all)
+            const uint32_t csh = MODE == 2 ? chunk_shift(p.ncols) : 0u;
             if (p.wide) {
-                SpanPass<uint32_t> mm;
+                SpanPass<uint32_t, MODE == 2> mm{csh};
                 rw.template each_group<false>(mm);
                 const uint32_t l = wave_min_u32(mm.l), h = wave_max_u32(mm.h);
+                if constexpr (MODE == 2) cmask = wave_or_u32(mm.cm);
                 lo = l;
                 hi = h;
                 if (l > h) {
@@ -926,6 +1103,8 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
             };
             if (!p.wide) {
                 window(std::true_type{}, 0u);
+            } else if constexpr (MODE == 2) {
+                for_windows(lo, hi, WIN, cmask, csh, [&](uint32_t wlo) { window(std::false_type{}, wlo); });
             } else {
                 for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) window(std::false_type{}, (uint32_t)wlo);
             }
@@ -940,7 +1119,10 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
 #define SLAT_NUM_ATTR
 #endif
 
-template <typename Sem, typename I, bool ELL>
+// MODE 0: every row by bitmap windows. Wide launches split the rows by output count (known from
+// symbolic): MODE 1 accumulates the rows with <= kHashT / 2 outputs in the LDS hash table and
+// skips the rest, MODE 2 takes the rest by row-span windows.
+template <typename Sem, typename I, bool ELL, int MODE = 0>
 __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     using S = typename Sem::S;
     using V = typename Sem::V;
@@ -951,7 +1133,10 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
     const NumLayout lay = num_layout(p.ww, p.area);
-    uint8_t *region = smem8 + (size_t)wv * lay.bytes;
+    // per-wave region: the bitmap window + rank slots, or (wide launches) the hash table in the
+    // same place
+    const uint32_t region_b = MODE == 1 ? hash_bytes<Sem>() : lay.bytes;
+    uint8_t *region = smem8 + (size_t)wv * region_b;
     uint2 *W = (uint2 *)region;
     uint32_t *L0 = (uint32_t *)region;  // L0[2w] aliases W[w].x
     uint8_t *slots = region + lay.off_slots;
@@ -971,8 +1156,17 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     const S bv0 = (S)bvmax;
     S *cval = (S *)p.c_val;
 
-    for (uint32_t w = lane; w < p.ww; w += kWave) W[w] = make_uint2(0u, 0u);
-    if (lane == 0) W[p.ww] = make_uint2(0u, 0x80000000u);  // dummy word: never set, never cleared
+    // hash table of the short-row path: keys | values | staged keys
+    uint32_t *hkeys = (uint32_t *)region;
+    V *hvals = (V *)(region + kHashT * 4);
+    uint32_t *hstage = (uint32_t *)(region + kHashT * 4 + kHashT * sizeof(V) * Sem::kSlots);
+    if constexpr (MODE == 1) {
+        for (uint32_t w = lane; w < kHashT; w += kWave) hkeys[w] = kSent;
+        for (uint32_t w = lane; w < kHashT * Sem::kSlots; w += kWave) hvals[w] = V(0);
+    } else {
+        for (uint32_t w = lane; w < p.ww; w += kWave) W[w] = make_uint2(0u, 0u);
+        if (lane == 0) W[p.ww] = make_uint2(0u, 0x80000000u);  // dummy word: never set, never cleared
+    }
     wave_sync();
 
     const uint32_t WIN = p.ww * 32;
@@ -988,17 +1182,79 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
         uint64_t out_pos = out_begin;
         uint32_t zeros = 0;
         ph[kPhaseSlots - 1] += 1;
-        if (a1 > a0) {
+        if constexpr (MODE != 0) {
+            if ((out_end - out_begin <= kHashT / 2) != (MODE == 1)) continue;  // the other launch's row
+        }
+        if constexpr (MODE == 1) {
+            // short row (its output count, known from symbolic, fits half the table)
+            if (a1 > a0) {
+            HashAcc<Sem> ha{hkeys, hvals};
+            if constexpr (Sem::kOrdered) {
+                traverse_ordered<I, S>(p, a0, a1, [&](uint32_t j, S a, S b) { ha.put(j, Sem::prod(a, b)); });
+            } else {
+                RowWalker<Sem, I, ELL, kVals> rw(p, a0, a1);
+                rw.template each_group<true>(ha);
+            }
+            wave_sync();
+            // the keys each lane holds (slots lane, lane + 64, ...), staged compacted for all lanes
+            uint32_t hk[kHashHeld], nh = 0;
+            sfor<kHashHeld>([&](auto I_) {
+                hk[I_] = hkeys[I_ * kWave + lane];
+                nh += hk[I_] != kSent ? 1u : 0u;
+            });
+            const uint32_t incl = wave_incl_scan(nh, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+            const uint32_t tot = readlane_u32(incl, kWave - 1);
+            uint32_t at = incl - nh;
+            sfor<kHashHeld>([&](auto I_) {
+                if (hk[I_] != kSent) hstage[at++] = hk[I_];
+            });
+            if (lane < 4) hstage[tot + lane] = kSent;  // pad for the 16-byte reads
+            wave_sync();
+            // rank = number of the row's keys below the held key (all keys distinct)
+            uint32_t rk[kHashHeld];
+            sfor<kHashHeld>([&](auto I_) { rk[I_] = 0; });
+            const uint4 *st4 = (const uint4 *)hstage;
+            for (uint32_t b = 0; b < tot; b += 4) {
+                const uint4 q = st4[b >> 2];
+                sfor<kHashHeld>([&](auto I_) {
+                    const uint32_t k = hk[I_];
+                    rk[I_] += (q.x < k) + (q.y < k) + (q.z < k) + (q.w < k);
+                });
+            }
+            uint32_t *oc = p.c_col + out_begin;
+            S *ov = cval + out_begin;
+            const uint64_t lim = out_end - out_begin;
+            sfor<kHashHeld>([&](auto I_) {
+                if (hk[I_] != kSent) {
+                    const uint32_t sl = I_ * kWave + lane;
+                    const S v = Sem::finish(hvals, sl);
+                    zeros += Sem::is_zero(v) ? 1u : 0u;
+                    if (rk[I_] < lim) {  // never write past the row's slice
+                        oc[rk[I_]] = hk[I_];
+                        ov[rk[I_]] = v;
+                    }
+                    hkeys[sl] = kSent;  // leave the table clean
+#pragma unroll
+                    for (int w = 0; w < Sem::kSlots; ++w) hvals[sl * Sem::kSlots + w] = V(0);
+                }
+            });
+            out_pos += tot;
+            wave_sync();
+            }
+        } else if (a1 > a0) {
             RowWalker<Sem, I, ELL, kVals> rw(p, a0, a1);
             const uint64_t len = rw.len;
             if constexpr (SLAT_PHASES) pin(rw.kq[0]);  // wait for the A entries inside phase 0
             mark(0);  // row bounds + A entries, group counts, tail compaction
             auto each_group = [&](auto &&grp, auto vals_tag) { rw.template each_group<decltype(vals_tag)::value>(grp); };
             uint64_t lo = 0, hi = p.ncols - 1;
+            uint32_t cmask = 0xFFFFFFFFu;  // touched column chunks (MODE 2 only; else all)
+            const uint32_t csh = MODE == 2 ? chunk_shift(p.ncols) : 0u;
             if (p.wide) {
-                SpanPass<S> mm;
+                SpanPass<S, MODE == 2> mm{csh};
                 each_group(mm, std::false_type{});
                 const uint32_t l = wave_min_u32(mm.l), h = wave_max_u32(mm.h);
+                if constexpr (MODE == 2) cmask = wave_or_u32(mm.cm);
                 lo = l;
                 hi = h;
                 if (l > h) {
@@ -1151,6 +1407,8 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
             };
             if (!p.wide) {
                 window(std::true_type{}, 0u);
+            } else if constexpr (MODE == 2) {
+                for_windows(lo, hi, WIN, cmask, csh, [&](uint32_t wlo) { window(std::false_type{}, wlo); });
             } else {
                 for (uint64_t wlo64 = lo & ~31ull; wlo64 <= hi; wlo64 += WIN) window(std::false_type{}, (uint32_t)wlo64);
             }
