@@ -262,6 +262,15 @@ template <typename Sem>
 static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
     // wide launches: the hash category (a.hash == 1) and the window category (a.hash == 2) are
     // instances of their own, so neither path's registers burden the other
+    if (a.hash == 3) {  // batched short rows (integer semirings, ELL B)
+        if constexpr (!Sem::kOrdered) {
+            if (idx32)
+                hipLaunchKernelGGL((k_numeric_short<Sem, uint32_t>), grid, dim3(kBlock), lds, s, a);
+            else
+                hipLaunchKernelGGL((k_numeric_short<Sem, uint64_t>), grid, dim3(kBlock), lds, s, a);
+        }
+        return hipGetLastError();
+    }
     if (a.hash == 1) {
         if (idx32 && ell)
             hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true, 1>), grid, dim3(kBlock), lds, s, a);
@@ -300,14 +309,19 @@ static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hi
 template <typename Sem>
 static int numeric_blocks_per_cu(bool idx32, bool ell, int mode, size_t lds) {
     // cached per (instance, LDS size): the query costs microseconds of host time per call
-    static thread_local int cache_nb[12] = {};
-    static thread_local size_t cache_lds[12] = {};
+    static thread_local int cache_nb[16] = {};
+    static thread_local size_t cache_lds[16] = {};
     const int ci = (idx32 ? 1 : 0) | (ell ? 2 : 0) | (mode << 2);
     if (cache_lds[ci] == lds && cache_nb[ci] > 0) return cache_nb[ci];
     int nb = 0;
     hipError_t e;
     auto occ = [&](auto kern) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kBlock, lds); };
-    if (mode == 1)
+    if (mode == 3) {
+        if constexpr (!Sem::kOrdered)
+            e = idx32 ? occ(k_numeric_short<Sem, uint32_t>) : occ(k_numeric_short<Sem, uint64_t>);
+        else
+            e = hipErrorInvalidValue;
+    } else if (mode == 1)
         e = idx32 ? (ell ? occ(k_numeric<Sem, uint32_t, true, 1>) : occ(k_numeric<Sem, uint32_t, false, 1>))
                   : (ell ? occ(k_numeric<Sem, uint64_t, true, 1>) : occ(k_numeric<Sem, uint64_t, false, 1>));
     else if (mode == 2)
@@ -500,8 +514,16 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (const char *e_ = std::getenv("SLAT_CAP")) a.area = 6 * std::max(64, std::atoi(e_));  // tuning knob
     a.area = (a.area + 15) & ~15u;
     const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.area).bytes;
-    const size_t hash_lds = (size_t)wpb * (dt == SLAT_U32     ? hash_bytes<SemU32>()
-                                           : dt == SLAT_SAT64 ? hash_bytes<SemSat64>()
+    // short rows batched several per hash table (integer semirings with the ELL copy of B), else
+    // one row per table; composite (row, column) keys need the column bits + 6 <= 31
+    const bool batched = hash && ell && dt != SLAT_F64 && !std::getenv("SLAT_NO_BATCH");
+    if (batched) {
+        uint32_t cb = 1;
+        while (cb < 64 && ((ncols - 1) >> cb)) ++cb;
+        a.cbits = cb <= 25 ? cb : 0;
+    }
+    const size_t hash_lds = (size_t)wpb * (dt == SLAT_U32     ? (batched ? short_bytes<SemU32>() : hash_bytes<SemU32>())
+                                           : dt == SLAT_SAT64 ? (batched ? short_bytes<SemSat64>() : hash_bytes<SemSat64>())
                                                               : hash_bytes<SemF64>());
     if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
     const size_t sym_lds = (size_t)wpb * asym.ww * 4, sym_hash_lds = (size_t)wpb * kSymHashT * 4;
@@ -514,7 +536,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc)));
     };
     const dim3 grid = num_grid(hash ? 2 : 0, num_lds);
-    const dim3 hash_grid = hash ? num_grid(1, hash_lds) : dim3(1);
+    const dim3 hash_grid = hash ? num_grid(batched ? 3 : 1, hash_lds) : dim3(1);
     const bool timing = flags & SLAT_FLAG_TIMING;
 
     // workspace: counts [n] | ablation counts [n] | shards | scan temp | ELL cols | ELL vals | ELL groups
@@ -652,7 +674,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     if (hash) {
         Args h1 = a;
-        h1.hash = 1;
+        h1.hash = batched ? 3 : 1;
         a.hash = 2;
         hipError_t he;
         if (dt == SLAT_U32) he = launch_numeric<SemU32>(idx32, ell, hash_grid, hash_lds, s, h1);

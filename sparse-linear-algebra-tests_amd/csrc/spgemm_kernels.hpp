@@ -96,7 +96,8 @@ struct Args {
     // MAGNUS-style short-row category (wide launches): rows whose outputs fit a per-wave LDS hash
     // table accumulate there and emit by rank-by-count instead of bitmap windows (0 = off)
     uint32_t hash;
-    uint32_t b_maxrow;  // max row length of B (the symbolic pass's product bound: len(A row) * b_maxrow)
+    uint32_t b_maxrow;
+    uint32_t cbits;     // k_numeric_short: column bits of the composite (row, column) keys (0: one row per batch)  // max row length of B (the symbolic pass's product bound: len(A row) * b_maxrow)
     unsigned long long *host_out;  // mapped pinned host words: [0] nnz, [1] max row nnz, [2] rows with zeros
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
@@ -1427,6 +1428,248 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
         }
     }
     // rows that lost explicit zeros (rare): counted straight into the mapped host word
+    if (lane == 0 && zrows)
+        __hip_atomic_fetch_add(&p.host_out[2], (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Short rows of wide launches, batched (MAGNUS's small-row category, integer semirings, ELL B).
+// A wave takes a tile of 64 consecutive rows and packs runs of consecutive short rows into batches
+// of <= kHashT / 2 outputs and <= 256 A entries: one hash table holds the whole batch under
+// composite keys (local row << cbits | column), so one dependent load chain and one rank pass
+// serve several rows, and every lane has work. Rank-by-count over composite keys is the order of
+// (row, column), i.e. the offset from the batch's first output: rows are contiguous in C.
+// Rows with more outputs belong to the window launch (MODE 2) and are skipped here.
+// ------------------------------------------------------------------------------------------------
+// LDS of k_numeric_short per wave: the hash table (hash_bytes) | entry -> row markers u32[256] |
+// per-row zero counts u32[64] | row order: slot of each staged key u32[256], row offsets u32[65],
+// row fill counters u32[64]
+template <typename Sem>
+__host__ __device__ constexpr uint32_t short_bytes() {
+    return hash_bytes<Sem>() + 256 * 4 + kWave * 4 + 256 * 4 + 68 * 4 + kWave * 4;
+}
+
+// Emit of a batch of rows held in the hash table: keys are staged grouped by row (rowoff[lr] +
+// a per-row counter), and a key's output position is rowoff[lr] + the number of keys of ITS row
+// below it (16-byte reads of the row's staged keys; composite keys of earlier rows are all
+// smaller, later rows' all larger, so reads may overrun the row's bounds). Keys are composite
+// (lr << cb | column) when cb > 0. The table, the counters are left clean; zero values go to
+// zero(local row).
+template <typename Sem, typename Z>
+__device__ __forceinline__ void batch_emit(uint32_t *hkeys, typename Sem::V *hvals, uint32_t *hstage, uint32_t *hslot,
+                                           const uint32_t *rowoff, uint32_t *rowctr, uint32_t cb, uint32_t tot,
+                                           uint32_t *oc, typename Sem::S *ov, Z &&zero) {
+    using S = typename Sem::S;
+    using V = typename Sem::V;
+    const int lane = lane_id();
+    sfor<kHashHeld>([&](auto I_) {
+        const uint32_t sl = I_ * kWave + lane;
+        const uint32_t k = hkeys[sl];
+        if (k != kSent) {
+            const uint32_t lr = cb ? k >> cb : 0u;
+            const uint32_t pos = rowoff[lr] + atomicAdd(&rowctr[lr], 1u);
+            if (pos < tot) {
+                hstage[pos] = k;
+                hslot[pos] = sl;
+            }
+            hkeys[sl] = kSent;
+        }
+    });
+    if (lane < 4) hstage[tot + lane] = kSent;  // pad for the 16-byte reads
+    wave_sync();
+    const uint32_t cmask = cb ? (1u << cb) - 1 : 0xFFFFFFFFu;
+    const uint4 *st4 = (const uint4 *)hstage;
+#pragma unroll
+    for (int m = 0; m < (int)(kHashT / 2 / kWave); ++m) {
+        const uint32_t j = m * kWave + lane;
+        if (j < tot) {
+            const uint32_t k = hstage[j], sl = hslot[j];
+            const uint32_t lr = cb ? k >> cb : 0u;
+            const uint32_t ro = rowoff[lr], re = rowoff[lr + 1];
+            uint32_t rk = 0;
+            for (uint32_t x = ro & ~3u; x < re; x += 4) {
+                const uint4 q = st4[x >> 2];
+                rk += (q.x < k) + (q.y < k) + (q.z < k) + (q.w < k);
+            }
+            rk += ro & ~3u;  // keys before the first read: all of earlier rows, all smaller
+            const S v = Sem::finish(hvals, sl);
+            if (Sem::is_zero(v)) zero(lr);
+            if (rk < tot) {
+                oc[rk] = k & cmask;
+                ov[rk] = v;
+            }
+#pragma unroll
+            for (int w = 0; w < Sem::kSlots; ++w) hvals[sl * Sem::kSlots + w] = V(0);
+        }
+    }
+    if (lane < 64) rowctr[lane] = 0;
+    wave_sync();
+}
+
+template <typename Sem, typename I>
+__global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
+    using S = typename Sem::S;
+    using V = typename Sem::V;
+    static_assert(!Sem::kOrdered, "f64 keeps the ordered single-row path");
+    constexpr int kWpb = kBlock / kWave;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
+    const int lane = lane_id();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    uint8_t *region = smem8 + (size_t)wv * short_bytes<Sem>();
+    uint32_t *hkeys = (uint32_t *)region;
+    V *hvals = (V *)(region + kHashT * 4);
+    uint32_t *hstage = (uint32_t *)(region + kHashT * 4 + kHashT * sizeof(V) * Sem::kSlots);
+    uint32_t *marks = (uint32_t *)(region + hash_bytes<Sem>());
+    uint32_t *zc = marks + 256;
+    uint32_t *hslot = zc + kWave, *rowoff = hslot + 256, *rowctr = rowoff + 68;
+    for (uint32_t w = lane; w < kHashT; w += kWave) hkeys[w] = kSent;
+    for (uint32_t w = lane; w < kHashT * Sem::kSlots; w += kWave) hvals[w] = V(0);
+    for (uint32_t w = lane; w < 256; w += kWave) marks[w] = 0;
+    zc[lane] = 0;
+    rowctr[lane] = 0;
+    wave_sync();
+    // pattern B (every B value equal): no B-value loads (u32 with the ELL copy, as k_numeric)
+    uint32_t bvmax = 0;
+    bool buni = false;
+    if constexpr (Sem::kNarrowable)
+        if (p.b_vmax) {
+            const unsigned long long v = ((volatile unsigned long long *)p.b_vmax)[kVMaxWord];
+            const unsigned long long vi = ((volatile unsigned long long *)p.b_vmax)[kVMinInvWord];
+            if ((uint32_t)(v >> 32) == p.epoch) {
+                bvmax = (uint32_t)v;
+                buni = (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax;
+            }
+        }
+    const S bv0 = (S)bvmax;
+    const S *av_ = (const S *)p.a_val;
+    S *cval = (S *)p.c_val;
+    uint32_t zrows = 0;
+    const uint32_t cb = p.cbits;
+    const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
+    for (uint64_t tile = (uint64_t)blockIdx.x * kWpb + wv; tile < ntiles; tile += (uint64_t)gridDim.x * kWpb) {
+        const uint64_t r0 = tile * kWave, r = r0 + lane;
+        const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
+        uint64_t A0j = 0, A1j = 0, obj = 0, oej = 0;
+        if ((uint32_t)lane < nt) {
+            A0j = p.a_rp[r];
+            A1j = p.a_rp[r + 1];
+            obj = p.c_rp[r];
+            oej = p.c_rp[r + 1];
+        }
+        const uint64_t uj = oej - obj, lj = A1j - A0j;
+        const bool shortj = (uint32_t)lane < nt && uj <= kHashT / 2;
+        const unsigned long long shortm = __ballot(shortj);
+        uint32_t b = 0;
+        for (;;) {
+            const unsigned long long m = b < (uint32_t)kWave ? (shortm >> b) << b : 0ull;
+            if (!m) break;
+            b = (uint32_t)__builtin_ctzll(m);
+            // the batch: short rows b, b+1, ... while outputs <= kHashT / 2 and entries <= 256
+            const bool inb = (uint32_t)lane >= b;
+            const uint32_t uu = inb ? (uint32_t)min<uint64_t>(uj, 1u << 20) : 0u;
+            const uint32_t ll = inb ? (uint32_t)min<uint64_t>(lj, 1u << 20) : 0u;
+            const uint32_t pu = wave_incl_scan(uu, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+            const uint32_t pl = wave_incl_scan(ll, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+            const unsigned long long stop = __ballot(inb && (!shortj || pu > kHashT / 2 || pl > 256 ||
+                                                             (cb == 0 && (uint32_t)lane > b)));
+            const uint32_t e = stop ? (uint32_t)__builtin_ctzll(stop) : nt;
+            const uint64_t A0 = readlane_u64(A0j, (int)b);
+            const uint64_t OB = readlane_u64(obj, (int)b);
+            HashAcc<Sem> ha{hkeys, hvals};
+            uint32_t lim;
+            if (e == b) {
+                // one short row with more than 256 entries: the walker, one segment at a time
+                const uint64_t A1 = readlane_u64(A1j, (int)b);
+                lim = (uint32_t)readlane_u64(uj, (int)b);
+                RowWalker<Sem, I, true, true> rw(p, (I)A0, (I)A1);
+                rw.template each_group<true>(ha);
+                if (lane == 0) {
+                    rowoff[0] = 0;
+                    rowoff[1] = lim;
+                }
+                wave_sync();
+                batch_emit<Sem>(hkeys, hvals, hstage, hslot, rowoff, rowctr, 0u, lim, p.c_col + OB, cval + OB,
+                                [&](uint32_t) { atomicAdd(&zc[0], 1u); });
+                if ((uint32_t)lane == b) {
+                    const uint32_t z = zc[0];
+                    p.counts[r] = uj - z;
+                    zrows += z ? 1u : 0u;
+                    zc[0] = 0;
+                }
+                ++b;
+                wave_sync();
+                continue;
+            }
+            const uint64_t A1 = readlane_u64(A1j, (int)(e - 1));
+            const uint32_t nent = (uint32_t)(A1 - A0);
+            lim = readlane_u32(pu, (int)(e - 1));
+            // entry -> local row: mark each row's first entry (a later, non-empty row wins a tie
+            // with empty rows before it), then a running max over the entries
+            if (inb && (uint32_t)lane < e && lj > 0) atomicMax(&marks[(uint32_t)(A0j - A0)], (uint32_t)lane - b + 1);
+            wave_sync();
+            uint32_t kq[kRegQ], lq[kRegQ], ng[kRegQ];
+            S aq[kRegQ];
+            uint32_t carry = 0, mxg = 0;
+            sfor<kRegQ>([&](auto Q) {
+                const uint32_t i = Q * kWave + lane;
+                const uint32_t mk = i < nent ? marks[i] : 0u;
+                const uint32_t run = max(wave_incl_scan(mk, 0u, [](uint32_t x, uint32_t y) { return max(x, y); }), carry);
+                carry = readlane_u32(run, kWave - 1);
+                lq[Q] = run - 1;
+                kq[Q] = kSent;
+                aq[Q] = S(0);
+                if (i < nent) {
+                    kq[Q] = p.a_col[A0 + i];
+                    aq[Q] = av_[A0 + i];
+                    marks[i] = 0;
+                }
+            });
+            sfor<kRegQ>([&](auto Q) {
+                if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
+                ng[Q] = kq[Q] != kSent ? p.ell_ng[kq[Q]] : 0u;
+                mxg = max(mxg, ng[Q]);
+            });
+            mxg = wave_max_u32(mxg);
+            for (uint32_t t = 0; t < mxg; ++t) {
+                uint4 c[kRegQ];
+                Quad<S> pv[kRegQ];
+                sfor<kRegQ>([&](auto Q) {
+                    c[Q] = make_uint4(kSent, kSent, kSent, kSent);
+                    pv[Q] = Quad<S>{};
+                    if (t < ng[Q]) {
+                        c[Q] = ell_cols(p, kq[Q], t);
+                        if (!buni) pv[Q] = ell_vals<S>(p, kq[Q], t);
+                    }
+                });
+                sfor<kRegQ>([&](auto Q) {
+                    const Quad<S> pr = buni ? splat4(Sem::prod(aq[Q], bv0)) : prods<Sem>(aq[Q], pv[Q]);
+                    const uint32_t hi = lq[Q] << cb;
+                    uint4 ck = c[Q];
+                    ck.x = ck.x != kSent ? (hi | ck.x) : kSent;
+                    ck.y = ck.y != kSent ? (hi | ck.y) : kSent;
+                    ck.z = ck.z != kSent ? (hi | ck.z) : kSent;
+                    ck.w = ck.w != kSent ? (hi | ck.w) : kSent;
+                    ha(ck, pr);
+                });
+            }
+            // row offsets within the batch: exclusive prefix of the output counts
+            if (inb && (uint32_t)lane < e) rowoff[lane - b] = pu - uu;
+            if ((uint32_t)lane == e - 1) rowoff[e - b] = pu;
+            wave_sync();
+            batch_emit<Sem>(hkeys, hvals, hstage, hslot, rowoff, rowctr, cb, lim, p.c_col + OB, cval + OB,
+                            [&](uint32_t lr) { atomicAdd(&zc[lr], 1u); });
+            if (inb && (uint32_t)lane < e) {
+                const uint32_t z = zc[lane - b];
+                p.counts[r] = uj - z;
+                zrows += z ? 1u : 0u;
+            }
+            wave_sync();
+            if (inb && (uint32_t)lane < e) zc[lane - b] = 0;
+            wave_sync();
+            b = e;
+        }
+    }
+    zrows = wave_sum_u32(zrows);
     if (lane == 0 && zrows)
         __hip_atomic_fetch_add(&p.host_out[2], (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
