@@ -414,6 +414,17 @@ static void pick_window(uint64_t ncols, uint32_t threads, uint32_t max_ww, uint3
     ww = (uint32_t)(blocks * threads);
 }
 
+// End of a call: poll the stream instead of a blocking sync, whose wake-up adds microseconds to
+// every call (SLAT_BLOCKING_SYNC=1 restores the blocking wait)
+static hipError_t wait_stream(hipStream_t s) {
+    static const bool blocking = std::getenv("SLAT_BLOCKING_SYNC") != nullptr;
+    if (blocking) return hipStreamSynchronize(s);
+    hipError_t e;
+    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    return e;
+}
+
 extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
                                             uint64_t row_end, const slat_csr_view *B, slat_csr *C, uint32_t flags) {
     if (!ctx || !C) return SLAT_EINVAL;
@@ -516,8 +527,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.area).bytes;
     // short rows batched several per hash table (integer semirings with the ELL copy of B), else
     // one row per table; composite (row, column) keys need the column bits + 6 <= 31
-    const bool batched = hash && ell && dt != SLAT_F64 && !std::getenv("SLAT_NO_BATCH");
-    if (batched) {
+    // symbolic batches for every value type (it never reads values); numeric for the integer ones
+    const bool sym_batched = hash && ell && !std::getenv("SLAT_NO_BATCH");
+    const bool batched = sym_batched && dt != SLAT_F64;
+    if (sym_batched) {
         uint32_t cb = 1;
         while (cb < 64 && ((ncols - 1) >> cb)) ++cb;
         a.cbits = cb <= 25 ? cb : 0;
@@ -557,7 +570,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
-    if ((st = slat_ensure_ws(ctx, o_smask + smask_b))) return st;
+    // batched wide launches: row product bounds u32[n] | symbolic / numeric window-row lists u32[n]
+    // | their counters
+    const size_t o_rb = o_smask + smask_b, rb_b = sym_batched ? up256(n * 4) : 0;
+    const size_t o_l1 = o_rb + rb_b, o_l2 = o_l1 + rb_b, o_lc = o_l2 + rb_b, lc_b = sym_batched ? 256 : 0;
+    if ((st = slat_ensure_ws(ctx, o_lc + lc_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (ell) {
         a.ell_wq = (uint32_t)wq;
@@ -628,7 +645,31 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
     }
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
-    if (hash) {
+    if (sym_batched) {
+        // MAGNUS categorisation: product bound per row, then the short rows batched in hash tables
+        // (listing the rest), then the listed rows by windows
+        unsigned int *lc = (unsigned int *)(ws + o_lc);
+        SLAT_HIP(ctx, hipMemsetAsync(lc, 0, lc_b, s));
+        uint32_t *rb = (uint32_t *)(ws + o_rb);
+        hipLaunchKernelGGL(k_row_bound, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kBlock - 1) / kBlock, ctx->cu_count * 8ull))),
+                           dim3(kBlock), 0, s, a.a_rp, a.a_col, n, a.b_nrows, a.ell_ng, rb);
+        SLAT_HIP(ctx, hipGetLastError());
+        Args h1 = asym, h2 = asym;
+        h1.rbound = rb;
+        h1.cbits = a.cbits;
+        h1.list = h2.list = (uint32_t *)(ws + o_l1);
+        h1.list_cnt = h2.list_cnt = lc;
+        h2.hash = 2;
+        const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kWave - 1) / kWave / wpb + 1, ctx->cu_count * 16ull)));
+        if (idx32)
+            hipLaunchKernelGGL(k_symbolic_short<uint32_t>, g1, dim3(kBlock), wpb * sym_short_bytes(), s, h1);
+        else
+            hipLaunchKernelGGL(k_symbolic_short<uint64_t>, g1, dim3(kBlock), wpb * sym_short_bytes(), s, h1);
+        SLAT_HIP(ctx, hipGetLastError());
+        launch_symbolic(idx32, ell, sym_grid, sym_lds, s, h2);
+        a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
+        a.list_cnt = lc + 16;
+    } else if (hash) {
         Args h1 = asym, h2 = asym;
         h1.hash = 1;
         h2.hash = 2;
@@ -676,6 +717,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         Args h1 = a;
         h1.hash = batched ? 3 : 1;
         a.hash = 2;
+        if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
         hipError_t he;
         if (dt == SLAT_U32) he = launch_numeric<SemU32>(idx32, ell, hash_grid, hash_lds, s, h1);
         else if (dt == SLAT_SAT64) he = launch_numeric<SemSat64>(idx32, ell, hash_grid, hash_lds, s, h1);
@@ -686,7 +728,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
     if (a.stats) SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                              hipMemcpyDeviceToHost, s));
-    SLAT_HIP(ctx, hipStreamSynchronize(s));
+    SLAT_HIP(ctx, wait_stream(s));
     if (SLAT_PHASES) {
         // diagnostic build: per-phase cycles of the numeric kernel, summed over waves
         unsigned long long ph[kPhaseSlots * 64];

@@ -97,7 +97,12 @@ struct Args {
     // table accumulate there and emit by rank-by-count instead of bitmap windows (0 = off)
     uint32_t hash;
     uint32_t b_maxrow;
-    uint32_t cbits;     // k_numeric_short: column bits of the composite (row, column) keys (0: one row per batch)  // max row length of B (the symbolic pass's product bound: len(A row) * b_maxrow)
+    uint32_t cbits;     // k_*_short: column bits of the composite (row, column) keys (0: one row per batch)
+    const uint32_t *rbound;  // k_symbolic_short: product bound per row (k_row_bound)
+    // rows of the window category, appended by the short-row kernels (symbolic / numeric lists)
+    // and walked by the MODE 2 launches instead of every row
+    uint32_t *list;
+    unsigned int *list_cnt;  // max row length of B (the symbolic pass's product bound: len(A row) * b_maxrow)
     unsigned long long *host_out;  // mapped pinned host words: [0] nnz, [1] max row nnz, [2] rows with zeros
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
@@ -1037,10 +1042,13 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     const uint32_t WIN = p.ww * 32;
     unsigned long long flops = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
-    for (uint64_t row = (uint64_t)blockIdx.x * kWpb + wv; row < p.nrows; row += stride) {
+    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
+    const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
+    for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
+        const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         if constexpr (MODE != 0) {
-            if (sym_short_row((uint64_t)(a1 - a0), p.b_maxrow) != (MODE == 1)) continue;  // the other launch's row
+            if (!listed && sym_short_row((uint64_t)(a1 - a0), p.b_maxrow) != (MODE == 1)) continue;  // the other launch's row
         }
         uint64_t cnt = 0;
         if constexpr (MODE == 1) {
@@ -1167,6 +1175,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     } else {
         for (uint32_t w = lane; w < p.ww; w += kWave) W[w] = make_uint2(0u, 0u);
         if (lane == 0) W[p.ww] = make_uint2(0u, 0x80000000u);  // dummy word: never set, never cleared
+        for (uint32_t w = lane; w < p.area / 4; w += kWave) ((uint32_t *)slots)[w] = 0;  // emit keeps it zero
     }
     wave_sync();
 
@@ -1177,7 +1186,10 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
     auto mark = [&](int i) { pc.mark(i); };
     uint64_t *ph = pc.ph;
-    for (uint64_t row = (uint64_t)blockIdx.x * kWpb + wv; row < p.nrows; row += stride) {
+    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
+    const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
+    for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
+        const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         const uint64_t out_begin = p.c_rp[row], out_end = p.c_rp[row + 1];
         uint64_t out_pos = out_begin;
@@ -1336,9 +1348,8 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                     VS *vals = (VS *)slots;
                     uint16_t *cols = (uint16_t *)(slots + ((cap * kVW * sizeof(VS) + 3) & ~3u));
                     const uint32_t nch = min(cap, wcnt - r0);
-                    for (uint32_t t = lane; t < nch * kVW; t += kWave) vals[t] = VS(0);
-                    wave_sync();
-                    mark(8);  // zero value slots
+                    // (the slots are zero: the previous chunk's emit cleared what it used)
+                    mark(8);
                     // 3. values and the column offset of every rank (duplicates store the same)
                     if constexpr (Sem::kOrdered) {
                         if (!(p.ablate & 8u))
@@ -1372,9 +1383,15 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                             v = (S)vals[t];
                         else
                             v = Sem::finish((const V *)vals, t);
+                        const uint32_t col = cols[t];
+                        // leave the slot area zero for the next chunk (values and column offsets):
+                        // no separate zeroing pass before the accumulate
+#pragma unroll
+                        for (uint32_t w = 0; w < kVW; ++w) vals[t * kVW + w] = VS(0);
+                        cols[t] = 0;
                         zeros += Sem::is_zero(v) ? 1u : 0u;
                         if (t < lim && !(p.ablate & 16u)) {  // never write past the row's slice
-                            oc[t] = wlo + cols[t];
+                            oc[t] = wlo + col;
                             ov[t] = v;
                         }
                     }
@@ -1441,6 +1458,149 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
 // (row, column), i.e. the offset from the batch's first output: rows are contiguous in C.
 // Rows with more outputs belong to the window launch (MODE 2) and are skipped here.
 // ------------------------------------------------------------------------------------------------
+// append row r of the lanes with `take` to p.list (one atomic per wave)
+__device__ __forceinline__ void list_rows(const Args &p, bool take, uint64_t r) {
+    if (!p.list) return;
+    const unsigned long long m = __ballot(take);
+    if (!m) return;
+    unsigned int base = 0;
+    if (lane_id() == 0) base = atomicAdd(p.list_cnt, (unsigned int)__popcll(m));
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (take) p.list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)r;
+}
+
+// MAGNUS row categorisation input: an upper bound of the scalar products of every row of A*B,
+// 4 x the ELL groups of the B rows it references (one lane per row; group counts sit in L2)
+static __global__ __launch_bounds__(kBlock) void k_row_bound(const uint64_t *a_rp, const uint32_t *a_col, uint64_t nrows,
+                                                      uint64_t b_nrows, const uint8_t *ell_ng, uint32_t *bound) {
+    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < nrows; r += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t a0 = a_rp[r], a1 = a_rp[r + 1];
+        uint64_t g = 0;
+        for (uint64_t i = a0; i < a1; i += 8) {  // 8 independent loads per round
+            uint32_t k[8];
+#pragma unroll
+            for (int x = 0; x < 8; ++x) k[x] = i + x < a1 ? a_col[i + x] : 0xFFFFFFFFu;
+#pragma unroll
+            for (int x = 0; x < 8; ++x)
+                if (k[x] < b_nrows) g += ell_ng[k[x]];
+        }
+        bound[r] = (uint32_t)min<uint64_t>(4 * g, 0xFFFFFFFFull);
+    }
+}
+
+// Symbolic of the short rows of a wide launch, batched like k_numeric_short: tiles of 64 rows,
+// runs of consecutive rows with product bound <= 0.7 kSymHashT and <= 256 entries share one
+// table of composite keys; a fresh insert counts for its row. Other rows go to p.list.
+__host__ __device__ constexpr uint32_t sym_short_bytes() { return kSymHashT * 4 + 256 * 4 + kWave * 4; }
+
+template <typename I>
+__global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
+    constexpr int kWpb = kBlock / kWave;
+    constexpr uint32_t kCap = kSymHashT * 7 / 10;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const int lane = lane_id();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    uint32_t *keys = smem + (size_t)wv * (sym_short_bytes() / 4);
+    uint32_t *marks = keys + kSymHashT, *rcnt = marks + 256;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) p.c_rp[0] = 0;
+        if (threadIdx.x < kShards) {
+            p.shards[threadIdx.x * kShardStride + 1] = 0;
+            p.shards[threadIdx.x * kShardStride + 2] = 0;
+        }
+    }
+    for (uint32_t w = lane; w < kSymHashT; w += kWave) keys[w] = kSent;
+    for (uint32_t w = lane; w < 256; w += kWave) marks[w] = 0;
+    rcnt[lane] = 0;
+    wave_sync();
+    const uint32_t cb = p.cbits;
+    unsigned long long flops = 0;
+    const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
+    for (uint64_t tile = (uint64_t)blockIdx.x * kWpb + wv; tile < ntiles; tile += (uint64_t)gridDim.x * kWpb) {
+        const uint64_t r0 = tile * kWave, r = r0 + lane;
+        const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
+        uint64_t A0j = 0, A1j = 0;
+        uint32_t bj = 0;
+        if ((uint32_t)lane < nt) {
+            A0j = p.a_rp[r];
+            A1j = p.a_rp[r + 1];
+            bj = p.rbound[r];
+        }
+        const uint64_t lj = A1j - A0j;
+        const bool shortj = (uint32_t)lane < nt && bj <= kCap && lj <= 256;
+        const unsigned long long shortm = __ballot(shortj);
+        list_rows(p, (uint32_t)lane < nt && !shortj, r);
+        uint32_t b = 0;
+        for (;;) {
+            const unsigned long long m = b < (uint32_t)kWave ? (shortm >> b) << b : 0ull;
+            if (!m) break;
+            b = (uint32_t)__builtin_ctzll(m);
+            const bool inb = (uint32_t)lane >= b;
+            const uint32_t pb = wave_incl_scan(inb ? bj : 0u, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+            const uint32_t pl = wave_incl_scan(inb ? (uint32_t)lj : 0u, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+            const unsigned long long stop =
+                __ballot(inb && (!shortj || pb > kCap || pl > 256 || (cb == 0 && (uint32_t)lane > b)));
+            const uint32_t e = stop ? (uint32_t)__builtin_ctzll(stop) : nt;  // > b: row b is short
+            const uint64_t A0 = readlane_u64(A0j, (int)b), A1 = readlane_u64(A1j, (int)(e - 1));
+            const uint32_t nent = (uint32_t)(A1 - A0);
+            if (inb && (uint32_t)lane < e && lj > 0) atomicMax(&marks[(uint32_t)(A0j - A0)], (uint32_t)lane - b + 1);
+            wave_sync();
+            uint32_t kq[kRegQ], lq[kRegQ], ng[kRegQ], carry = 0, mxg = 0;
+            sfor<kRegQ>([&](auto Q) {
+                const uint32_t i = Q * kWave + lane;
+                const uint32_t mk = i < nent ? marks[i] : 0u;
+                const uint32_t run = max(wave_incl_scan(mk, 0u, [](uint32_t x, uint32_t y) { return max(x, y); }), carry);
+                carry = readlane_u32(run, kWave - 1);
+                lq[Q] = run - 1;
+                kq[Q] = kSent;
+                if (i < nent) {
+                    kq[Q] = p.a_col[A0 + i];
+                    marks[i] = 0;
+                }
+            });
+            sfor<kRegQ>([&](auto Q) {
+                if (kq[Q] >= p.b_nrows) kq[Q] = kSent;
+                ng[Q] = kq[Q] != kSent ? p.ell_ng[kq[Q]] : 0u;
+                mxg = max(mxg, ng[Q]);
+            });
+            mxg = wave_max_u32(mxg);
+            uint32_t nprod = 0;
+            for (uint32_t t = 0; t < mxg; ++t) {
+                uint4 c[kRegQ];
+                sfor<kRegQ>([&](auto Q) {
+                    c[Q] = make_uint4(kSent, kSent, kSent, kSent);
+                    if (t < ng[Q]) c[Q] = ell_cols(p, kq[Q], t);
+                });
+                sfor<kRegQ>([&](auto Q) {
+                    const uint32_t hi = lq[Q] << cb;
+                    uint32_t cc[4] = {c[Q].x, c[Q].y, c[Q].z, c[Q].w}, sl[4];
+                    bool fresh[4];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) {
+                        nprod += cc[x] != kSent ? 1u : 0u;
+                        cc[x] = cc[x] != kSent ? (hi | cc[x]) : kSent;
+                    }
+                    hash_batch<4>(keys, 10, cc, sl, fresh);
+                    const uint32_t f = (uint32_t)fresh[0] + fresh[1] + fresh[2] + fresh[3];
+                    if (f) atomicAdd(&rcnt[lq[Q]], f);
+                });
+            }
+            wave_sync();
+            if (p.stats) flops += wave_sum_u32(nprod);
+            if (inb && (uint32_t)lane < e) {
+                p.counts[r] = rcnt[lane - b];
+                rcnt[lane - b] = 0;
+            }
+            uint4 *k4 = (uint4 *)keys;
+            for (uint32_t w = lane; w < kSymHashT / 4; w += kWave) k4[w] = make_uint4(kSent, kSent, kSent, kSent);
+            wave_sync();
+            b = e;
+        }
+    }
+    if (p.stats && lane == 0 && flops)
+        atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
+}
+
 // LDS of k_numeric_short per wave: the hash table (hash_bytes) | entry -> row markers u32[256] |
 // per-row zero counts u32[64] | row order: slot of each staged key u32[256], row offsets u32[65],
 // row fill counters u32[64]
@@ -1559,6 +1719,7 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
         const uint64_t uj = oej - obj, lj = A1j - A0j;
         const bool shortj = (uint32_t)lane < nt && uj <= kHashT / 2;
         const unsigned long long shortm = __ballot(shortj);
+        list_rows(p, (uint32_t)lane < nt && !shortj, r);  // the window launch's rows
         uint32_t b = 0;
         for (;;) {
             const unsigned long long m = b < (uint32_t)kWave ? (shortm >> b) << b : 0ull;
