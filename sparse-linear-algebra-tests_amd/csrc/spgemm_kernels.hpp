@@ -51,6 +51,7 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_PHASES
 #define SLAT_PHASES 0  // diagnostic builds: per-phase s_memtime cycles of k_numeric
 #endif
+
 constexpr int kPhaseSlots = 16;  // [0..12] phases, [15] rows
 
 // diagnostic builds: s_memtime phase accumulator (compiled away otherwise)
@@ -746,8 +747,8 @@ struct RowWalker {
         single = nseg == 1;
         if (single) load_seg(a0);
     }
-
-    __device__ __forceinline__ void load_seg(I sb) {
+    // the A entries [sb, min(a1, sb + kSeg)) of a row, kRegQ per lane (kSent / 0 past the end)
+    __device__ static __forceinline__ void seg_loads(const Args &p, I sb, I a1, uint32_t *k, S *a) {
         const int lane = lane_id();
         const S *av_ = (const S *)p.a_val;
         // wave-uniform segment base + a 32-bit lane offset (SGPR-base addressing, no 64-bit math)
@@ -757,13 +758,23 @@ struct RowWalker {
         sfor<kRegQ>([&](auto Q) {
             constexpr int q = Q;
             const uint32_t j = (uint32_t)(q * kWave + lane);
-            kq[q] = kSent;
-            aq[q] = S(0);
+            k[q] = kSent;
+            a[q] = S(0);
             if (j < seg_n) {
-                kq[q] = seg_c[j];
-                if constexpr (AVALS) aq[q] = seg_v[j];
+                k[q] = seg_c[j];
+                if constexpr (AVALS) a[q] = seg_v[j];
             }
         });
+    }
+
+    __device__ __forceinline__ void load_seg(I sb) {
+        seg_loads(p, sb, a1, kq, aq);
+        finish_seg();
+    }
+
+    // group counts and the compacted tail batches of the segment in kq / aq
+    __device__ __forceinline__ void finish_seg() {
+        const int lane = lane_id();
         sfor<kRegQ>([&](auto Q) {
             if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
             if constexpr (Sem::kNarrowable) amax = max(amax, (uint32_t)aq[Q]);

@@ -110,7 +110,7 @@ def main():
     ap.add_argument("--cpu-max-nnz", type=float, default=3e7, help="skip the CPU leg above this nnz(A)")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
     ap.add_argument("--only", default="C1,C2,C3,C4,C5")
-    ap.add_argument("--rmat-scale", type=int, default=18)
+    ap.add_argument("--rmat-scale", type=int, default=16)
     ap.add_argument("--rmat-deg", type=int, default=16)
     args = ap.parse_args()
     only = set(args.only.split(","))
