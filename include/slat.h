@@ -54,6 +54,10 @@ typedef enum { SLAT_DEVICE = 0, SLAT_HOST = 1 } slat_residency;
 #define SLAT_FLAG_TIMING      0x1u  /* record per-kernel HIP events; read with slat_get_stats */
 #define SLAT_FLAG_EXACT_ALLOC 0x2u  /* size C exactly (extra mid-call sync) instead of by bound */
 #define SLAT_FLAG_STATS       0x4u  /* also count scalar products (flops) for slat_get_stats */
+/* f64 only: sum each output's products in any order (LDS / global atomics) instead of the
+ * reference's left fold in A-row order; results then agree with the reference within the stated
+ * tolerance (relative 1e-12 for same-sign values), not bit for bit (config C5). */
+#define SLAT_FLAG_F64_ANY_ORDER 0x8u
 
 typedef struct slat_ctx slat_ctx;
 

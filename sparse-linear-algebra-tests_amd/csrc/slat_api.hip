@@ -465,6 +465,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const uint64_t ncols = B->n_cols;
     const int32_t dt = A->dtype;
     const size_t vs = vsize(dt);
+    // f64 in any summation order (tolerance-checked, config C5) instead of the reference's fold order
+    const bool f64any = dt == SLAT_F64 && (flags & SLAT_FLAG_F64_ANY_ORDER);
     hipStream_t s = ctx->stream;
     C->n_rows = n;
     C->n_cols = ncols;
@@ -529,7 +531,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // one row per table; composite (row, column) keys need the column bits + 6 <= 31
     // symbolic batches for every value type (it never reads values); numeric for the integer ones
     const bool sym_batched = hash && ell && !std::getenv("SLAT_NO_BATCH");
-    const bool batched = sym_batched && dt != SLAT_F64;
+    const bool batched = sym_batched && (dt != SLAT_F64 || f64any);
     if (sym_batched) {
         uint32_t cb = 1;
         while (cb < 64 && ((ncols - 1) >> cb)) ++cb;
@@ -537,6 +539,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     const size_t hash_lds = (size_t)wpb * (dt == SLAT_U32     ? (batched ? short_bytes<SemU32>() : hash_bytes<SemU32>())
                                            : dt == SLAT_SAT64 ? (batched ? short_bytes<SemSat64>() : hash_bytes<SemSat64>())
+                                           : f64any           ? (batched ? short_bytes<SemF64Any>() : hash_bytes<SemF64Any>())
                                                               : hash_bytes<SemF64>());
     if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
     const size_t sym_lds = (size_t)wpb * asym.ww * 4, sym_hash_lds = (size_t)wpb * kSymHashT * 4;
@@ -545,6 +548,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     auto num_grid = [&](int mode, size_t lds) {
         const int nbpc = dt == SLAT_U32     ? numeric_blocks_per_cu<SemU32>(idx32, ell, mode, lds)
                          : dt == SLAT_SAT64 ? numeric_blocks_per_cu<SemSat64>(idx32, ell, mode, lds)
+                         : f64any           ? numeric_blocks_per_cu<SemF64Any>(idx32, ell, mode, lds)
                                             : numeric_blocks_per_cu<SemF64>(idx32, ell, mode, lds);
         return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc)));
     };
@@ -701,6 +705,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     auto launch_num = [&](const Args &x) -> hipError_t {
         if (dt == SLAT_U32) return launch_numeric<SemU32>(idx32, ell, grid, num_lds, s, x);
         if (dt == SLAT_SAT64) return launch_numeric<SemSat64>(idx32, ell, grid, num_lds, s, x);
+        if (f64any) return launch_numeric<SemF64Any>(idx32, ell, grid, num_lds, s, x);
         return launch_numeric<SemF64>(idx32, ell, grid, num_lds, s, x);
     };
     if (ablate & ~7u) {
@@ -721,6 +726,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         hipError_t he;
         if (dt == SLAT_U32) he = launch_numeric<SemU32>(idx32, ell, hash_grid, hash_lds, s, h1);
         else if (dt == SLAT_SAT64) he = launch_numeric<SemSat64>(idx32, ell, hash_grid, hash_lds, s, h1);
+        else if (f64any) he = launch_numeric<SemF64Any>(idx32, ell, hash_grid, hash_lds, s, h1);
         else he = launch_numeric<SemF64>(idx32, ell, hash_grid, hash_lds, s, h1);
         SLAT_HIP(ctx, he);
     }

@@ -171,6 +171,28 @@ struct SemF64 {
     __device__ static __forceinline__ bool is_zero(S v) { return v == 0.0; }
 };
 
+// f64 in any order (SLAT_FLAG_F64_ANY_ORDER; BASELINE config C5 is tolerance-checked): LDS atomic
+// adds like the integer semirings, so every traversal, category and batch applies; rows with more
+// outputs than the LDS slots accumulate straight into their C slice with global atomics instead of
+// re-traversing the row once per rank chunk (kGlobalOverflow).
+struct SemF64Any {
+    using S = double;
+    using P = double;
+    using V = double;
+    static constexpr int kSlots = 1;
+    static constexpr bool kOrdered = false;
+    static constexpr bool kNarrowable = false;
+    static constexpr bool kGlobalOverflow = true;
+    __device__ static __forceinline__ P prod(S a, S b) { return __dmul_rn(a, b); }
+    __device__ static __forceinline__ void acc(V *vals, uint32_t r, P p) { atomicAdd(&vals[r], p); }
+    __device__ static __forceinline__ S finish(const V *vals, uint32_t t) { return vals[t]; }
+    __device__ static __forceinline__ bool is_zero(S v) { return v == 0.0; }
+};
+template <typename Sem, typename = void>
+struct GlobalOverflow : std::false_type {};
+template <typename Sem>
+struct GlobalOverflow<Sem, std::void_t<decltype(Sem::kGlobalOverflow)>> : std::bool_constant<Sem::kGlobalOverflow> {};
+
 // compile-time loop: f(std::integral_constant<int, i>) for i in [0, N) — indices stay constants, so
 // register arrays indexed by them are never demoted to scratch
 template <typename F, int... Is>
@@ -243,7 +265,10 @@ __device__ __forceinline__ S readlane_val(S v, int l) {
 }
 
 // Ordered traversal (f64): A's row entries in order, lanes spread over one B row (distinct
-// columns), 64 A entries' row pointers prefetched at a time.
+// columns), 64 A entries' row pointers prefetched at a time. The first 64 elements of the B rows
+// of kOrdAhead consecutive entries are loaded before any of them is visited, so the visits (in A
+// order: the left fold of linalg/src/csr.rs:325-337) do not wait on one load chain per entry.
+constexpr int kOrdAhead = 8;
 template <typename I, typename S, typename F>
 __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&visit) {
     const int lane = lane_id();
@@ -262,10 +287,31 @@ __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&
             }
         }
         const int cnt = (int)min<uint64_t>((uint64_t)kWave, (uint64_t)(a1 - base));
-        for (int t = 0; t < cnt; ++t) {
-            const I s = (I)readlane_u64((uint64_t)bs, t), e = (I)readlane_u64((uint64_t)be, t);
-            const S a = readlane_val(av, t);
-            for (I jdx = s + (I)lane; jdx < e; jdx += (I)kWave) visit(p.b_col[jdx], a, bv_[jdx]);
+        for (int t0 = 0; t0 < cnt; t0 += kOrdAhead) {
+            uint32_t pc[kOrdAhead];
+            S pv[kOrdAhead];
+            sfor<kOrdAhead>([&](auto G) {
+                pc[G] = kSent;
+                pv[G] = S(0);
+                const int t = t0 + G;
+                if (t < cnt) {
+                    const I s = (I)readlane_u64((uint64_t)bs, t), e = (I)readlane_u64((uint64_t)be, t);
+                    const I jdx = s + (I)lane;
+                    if (jdx < e) {
+                        pc[G] = p.b_col[jdx];
+                        pv[G] = bv_[jdx];
+                    }
+                }
+            });
+            sfor<kOrdAhead>([&](auto G) {
+                const int t = t0 + G;
+                if (t < cnt) {
+                    const I s = (I)readlane_u64((uint64_t)bs, t), e = (I)readlane_u64((uint64_t)be, t);
+                    const S a = readlane_val(av, t);
+                    if (pc[G] != kSent) visit(pc[G], a, pv[G]);
+                    for (I jdx = s + (I)kWave + (I)lane; jdx < e; jdx += (I)kWave) visit(p.b_col[jdx], a, bv_[jdx]);
+                }
+            });
         }
     }
 }
@@ -432,6 +478,40 @@ __device__ __forceinline__ void walk_brow(const Args &p, uint32_t k, typename Se
     }
 }
 
+// CSR walk of N A entries per lane (k = B row, kSent = none): a B row of at most kLongB entries is
+// walked by its own lane, a longer one by the whole wave (lanes over its columns), so no lane walks
+// thousands of entries alone (power-law B rows).
+constexpr uint32_t kLongB = 32;
+template <typename Sem, bool VALS, typename I, int N, typename G>
+__device__ __forceinline__ void walk_csr(const Args &p, const uint32_t *k, const typename Sem::S *a, G &&grp) {
+    using S = typename Sem::S;
+    const int lane = lane_id();
+    const S *bv_ = (const S *)p.b_val;
+    I bs[N], be[N];
+    sfor<N>([&](auto Q) {
+        bs[Q] = 0;
+        be[Q] = 0;
+        if (k[Q] < p.b_nrows) {
+            bs[Q] = (I)p.b_rp[k[Q]];
+            be[Q] = (I)p.b_rp[k[Q] + 1];
+        }
+    });
+    sfor<N>([&](auto Q) {
+        if ((uint64_t)(be[Q] - bs[Q]) <= kLongB)
+            for (I jdx = bs[Q]; jdx < be[Q]; ++jdx)
+                grp(make_uint4(p.b_col[jdx], kSent, kSent, kSent), quad1<S>(VALS ? Sem::prod(a[Q], bv_[jdx]) : S(0)));
+    });
+    sfor<N>([&](auto Q) {
+        for (unsigned long long m = __ballot((uint64_t)(be[Q] - bs[Q]) > kLongB); m; m &= m - 1) {
+            const int l = (int)__builtin_ctzll(m);
+            const I s = (I)readlane_u64((uint64_t)bs[Q], l), e = (I)readlane_u64((uint64_t)be[Q], l);
+            const S av = readlane_val(a[Q], l);
+            for (I jdx = s + (I)lane; jdx < e; jdx += (I)kWave)
+                grp(make_uint4(p.b_col[jdx], kSent, kSent, kSent), quad1<S>(VALS ? Sem::prod(av, bv_[jdx]) : S(0)));
+        }
+    });
+}
+
 // Lane-per-A-entry walk of a row: lane l owns entries base + l and base + 64 + l.
 template <typename Sem, bool ELL, bool VALS, typename I, typename G>
 __device__ __forceinline__ void walk_row(const Args &p, I a0, I a1, G &&grp) {
@@ -440,18 +520,22 @@ __device__ __forceinline__ void walk_row(const Args &p, I a0, I a1, G &&grp) {
     const S *av_ = (const S *)p.a_val;
     for (I base = a0; base < a1; base += (I)(2 * kWave)) {
         const I i0 = base + (I)lane, i1 = i0 + (I)kWave;
-        uint32_t k0 = kSent, k1 = kSent;
-        S a0v = S(0), a1v = S(0);
+        uint32_t kk[2] = {kSent, kSent};
+        S av[2] = {S(0), S(0)};
         if (i0 < a1) {
-            k0 = p.a_col[i0];
-            if constexpr (VALS) a0v = av_[i0];
+            kk[0] = p.a_col[i0];
+            if constexpr (VALS) av[0] = av_[i0];
         }
         if (i1 < a1) {
-            k1 = p.a_col[i1];
-            if constexpr (VALS) a1v = av_[i1];
+            kk[1] = p.a_col[i1];
+            if constexpr (VALS) av[1] = av_[i1];
         }
-        if (k0 < p.b_nrows) walk_brow<Sem, ELL, VALS, I>(p, k0, a0v, 0, grp);
-        if (k1 < p.b_nrows) walk_brow<Sem, ELL, VALS, I>(p, k1, a1v, 0, grp);
+        if constexpr (ELL) {
+            if (kk[0] < p.b_nrows) walk_brow<Sem, ELL, VALS, I>(p, kk[0], av[0], 0, grp);
+            if (kk[1] < p.b_nrows) walk_brow<Sem, ELL, VALS, I>(p, kk[1], av[1], 0, grp);
+        } else {
+            walk_csr<Sem, VALS, I, 2>(p, kk, av, grp);
+        }
     }
 }
 
@@ -868,9 +952,7 @@ struct RowWalker {
                 if (nb > 1) grp(ct1, pt1);
             }
         } else if (single) {
-            sfor<kRegQ>([&](auto Q) {
-                if (kq[Q] != kSent) walk_brow<Sem, false, VV, I>(p, kq[Q], aq[Q], 0, grp);
-            });
+            walk_csr<Sem, VV, I, kRegQ>(p, kq, aq, grp);
         } else {
             walk_row<Sem, false, VV, I>(p, a0, a1, grp);
         }
@@ -1004,6 +1086,33 @@ struct AccPass {
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) { run<1>(&c, &pr); }
     __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
         sfor<kRegQ>([&](auto Q) { run<1>(c + Q, pr + Q); });
+    }
+};
+
+// accumulate straight into the row's C slice (kGlobalOverflow semirings, rows beyond the LDS
+// slots): global atomic add at out + rank, the column stored alongside (duplicates store the same)
+template <typename Sem>
+struct GlobalAcc {
+    using S = typename Sem::S;
+    const uint2 *W;
+    uint32_t ww, wlo, nrank;
+    uint32_t *oc;
+    S *ov;
+    __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) {
+        const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            uint32_t off;
+            const uint2 w = rank_word(W, ww, cc[e], wlo, off);
+            const uint32_t r = rank_in(w, off, 0u, nrank);
+            if (r != kSent) {
+                atomicAdd(&ov[r], pr.v[e]);
+                oc[r] = wlo + off;
+            }
+        }
+    }
+    __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
+        sfor<kRegQ>([&](auto Q) { (*this)(c[Q], pr[Q]); });
     }
 };
 
@@ -1413,6 +1522,28 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 auto run_chunks = [&](auto narrow_tag, auto uni_tag) {
                     constexpr bool NW = decltype(narrow_tag)::value;
                     const uint32_t cap = NW ? cap_n : cap_w;
+                    if constexpr (GlobalOverflow<Sem>::value) {
+                        if (wcnt > cap) {
+                            // one pass into the C slice: zero it, then global atomics at out + rank
+                            uint32_t *oc = p.c_col + out_pos;
+                            S *ov = cval + out_pos;
+                            const uint32_t lim = (uint32_t)min<uint64_t>(out_end - min(out_pos, out_end), wcnt);
+                            for (uint32_t t = lane; t < lim; t += kWave) ov[t] = S(0);
+                            __builtin_amdgcn_s_waitcnt(0);  // the zeros reach L2 before the atomics
+                            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                            GlobalAcc<Sem> ga{W, p.ww, Z ? 0u : wlo, lim, oc, ov};
+                            rw.template each_group<true>(ga);
+                            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+                            // zero sums (cancellation) are counted by the compaction test below
+                            for (uint32_t t = lane; t < lim; t += kWave) {
+                                const S v = __hip_atomic_load(&ov[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                zeros += Sem::is_zero(v) ? 1u : 0u;
+                            }
+                            out_pos += wcnt;
+                            wave_sync();
+                            return;
+                        }
+                    }
                     if (Z && wcnt <= cap) {  // the common case: one chunk from rank 0
                         chunk(narrow_tag, uni_tag, std::true_type{}, 0u, cap);
                     } else {
