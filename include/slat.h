@@ -9,6 +9,9 @@
  *   MagnusMatrix::matmul    src/graph_magnus.rs:224-232      slat_spgemm_csr_sat64
  *   MagnusMatrix::matmul_seq src/graph_magnus.rs:234-242     slat_spgemm_csr_sat64
  *   linalg Csr<u32,f64>::matmul{,_par} linalg/src/csr.rs:308-466  slat_spgemm_csr_f64
+ *   CsrMatrix::from_coo     src/graph_csr.rs:83-129          slat_csr_from_coo (device) / slat_host_from_coo
+ *   CsrMatrix::lattice      src/graph_csr.rs:177-222         slat_csr_lattice (device) / slat_host_lattice
+ *   CsrMatrix::thin         src/graph_csr.rs:225-247         slat_csr_thin (device) / slat_host_thin
  *   CsrMatrix::add          src/graph_csr.rs:487-542         slat_csr_add
  *   CsrMatrix::identity     src/graph_csr.rs:68-80           slat_csr_identity
  *   CsrMatrix::reachability_sum    src/graph_csr.rs:545-559  slat_reachability_sum
@@ -185,6 +188,23 @@ slat_status slat_host_thin(const slat_host_csr *m, slat_rng *rng, double density
 slat_status slat_host_rmat(uint32_t scale, uint64_t n_edges, double a, double b, double c,
                            const uint8_t seed[32], slat_host_csr *out);
 void slat_host_csr_free(slat_host_csr *m);
+
+/* --- the reference's constructors on the device ------------------------ */
+/* CsrMatrix::from_coo (src/graph_csr.rs:83-129): sort by (row, col), sum duplicates (u32 / u64
+ * wrapping like the reference's release build; f64 in input order), drop zeros. Triplet arrays
+ * rows, cols u32 and vals (u32 | u64 | f64 per dtype) are device or host memory per `residency`.
+ * A row or column id >= n -> SLAT_EINVAL (the reference panics on the index). */
+slat_status slat_csr_from_coo(slat_ctx *ctx, uint64_t n, uint64_t ntrip, const uint32_t *rows,
+                              const uint32_t *cols, const void *vals, int32_t dtype, int32_t residency,
+                              slat_csr *out);
+/* CsrMatrix::lattice (src/graph_csr.rs:177-222), built on the device (u32 values 1). */
+slat_status slat_csr_lattice(slat_ctx *ctx, const uint64_t *dims, int ndim, int torus, slat_csr *out);
+/* CsrMatrix::thin (src/graph_csr.rs:225-247) of a device matrix: the same draws as the host StdRng
+ * (one f64 per entry with row <= col, row-major order), each computed from its stream position;
+ * *rng ends where the reference's generator would. */
+slat_status slat_csr_thin(slat_ctx *ctx, const slat_csr_view *m, slat_rng *rng, double density,
+                          slat_csr *out);
+
 
 #ifdef __cplusplus
 }

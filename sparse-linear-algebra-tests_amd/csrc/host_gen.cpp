@@ -161,6 +161,30 @@ double slat_rng_next_f64(slat_rng *rng) {
     return (double)(slat_rng_next_u64(rng) >> 12) * (1.0 / 4503599627370496.0);
 }
 
+// Stream position of a StdRng (slat_internal.hpp): the key and the index of the next keystream word,
+// so a device generator can draw the same values; advance = `draws` u64 draws later, in the state the
+// host generator would be in after making them itself.
+void slat_rng_position(const slat_rng *rng, uint32_t key[8], uint64_t *word) {
+    const Rng *r = reinterpret_cast<const Rng *>(rng);
+    std::memcpy(key, r->key, 32);
+    *word = r->idx >= 64 ? r->counter * 16 : (r->counter - 4) * 16 + r->idx;
+}
+
+void slat_rng_advance(slat_rng *rng, uint64_t draws) {
+    Rng *r = R(rng);
+    uint32_t key[8];
+    uint64_t w;
+    slat_rng_position(rng, key, &w);
+    w += 2 * draws;
+    r->counter = (w / 64) * 4;
+    r->idx = 64;
+    if (w % 64) {  // mid-refill: the 4 blocks holding word w, read position inside them
+        for (int b = 0; b < 4; ++b) chacha12(r->key, r->counter + (uint64_t)b, r->buf + 16 * b);
+        r->counter += 4;
+        r->idx = (uint32_t)(w % 64);
+    }
+}
+
 void slat_host_csr_free(slat_host_csr *m) {
     if (!m) return;
     std::free(m->row_ptr);

@@ -74,3 +74,8 @@ slat_status slat_check_view(slat_ctx *ctx, const slat_csr_view *v, const char *n
 // rp[0..n] = exclusive prefix of counts[0..n) (rp[n] = total) by k_scan_rows on stream s; the total
 // and the max count land in ctx->h_out[0], [1] once the stream reaches that point
 slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s);
+
+// StdRng stream position (host_gen.cpp): key words and the index of the next keystream word; and
+// the host state after `draws` more u64 draws (device generators draw by position)
+extern "C" void slat_rng_position(const slat_rng *rng, uint32_t key[8], uint64_t *word);
+extern "C" void slat_rng_advance(slat_rng *rng, uint64_t draws);

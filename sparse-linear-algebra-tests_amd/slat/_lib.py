@@ -23,7 +23,7 @@ EXPORTS = [
     "slat_spgemm_csr_f64", "slat_spgemm_rowblock", "slat_rng_seed", "slat_rng_next_u64", "slat_rng_next_f64",
     "slat_host_from_coo", "slat_host_lattice", "slat_host_thin", "slat_host_rmat", "slat_host_csr_free",
     "slat_csr_add", "slat_csr_identity", "slat_csr_pattern_equal", "slat_reachability_sum",
-    "slat_power_until_stable", "slat_connected_components",
+    "slat_power_until_stable", "slat_connected_components", "slat_csr_from_coo", "slat_csr_lattice", "slat_csr_thin",
 ]
 
 
@@ -116,6 +116,9 @@ def lib():
         "slat_reachability_sum": ([vp, P(CsrView), P(CsrOwned), P(u64)], C.c_int),
         "slat_power_until_stable": ([vp, P(CsrView), P(CsrOwned), P(u64)], C.c_int),
         "slat_connected_components": ([vp, P(CsrView), vp], C.c_int),
+        "slat_csr_from_coo": ([vp, u64, u64, vp, vp, vp, i32, i32, P(CsrOwned)], C.c_int),
+        "slat_csr_lattice": ([vp, P(u64), C.c_int, C.c_int, P(CsrOwned)], C.c_int),
+        "slat_csr_thin": ([vp, P(CsrView), P(RngState), C.c_double, P(CsrOwned)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -175,6 +175,13 @@ def torus_thinned(side: int, epn: float, rng: StdRng) -> HostCsr:
     return host_thin(full, rng, density) if density < 1.0 else full
 
 
+def torus_thinned_device(side: int, epn: float, rng: StdRng, ctx: Context | None = None) -> "CsrMatrix":
+    """torus_thinned, generated on the device (lattice + thin kernels): same matrix, same draws."""
+    full = CsrMatrix.lattice([side, side, side], True, ctx)
+    density = epn / (full.nnz() / full.n)
+    return full.thin(rng, density) if density < 1.0 else full
+
+
 # ------------------------------------------------------------------------------------------------
 # device-resident matrices
 # ------------------------------------------------------------------------------------------------
@@ -248,11 +255,34 @@ class DeviceCsr:
         return cls.from_edges(len(names), edges), names
 
     @classmethod
-    def lattice(cls, dims: Sequence[int], torus: bool):
-        return cls.from_host(host_lattice(dims, torus))
+    def lattice(cls, dims: Sequence[int], torus: bool, ctx: Context | None = None):
+        """CsrMatrix::lattice (src/graph_csr.rs:177-222), built on the device (u32 values 1)."""
+        ctx = ctx or default_context()
+        d = (C.c_uint64 * len(dims))(*dims)
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_lattice(ctx.ptr, d, len(dims), int(torus), C.byref(out)), ctx.ptr)
+        m = CsrMatrix(out, ctx)
+        return m if cls.DTYPE == L.U32 else cls.from_host(m.host().astype(cls.DTYPE), ctx)
 
     def thin(self, rng: StdRng, density: float):
-        return type(self).from_host(host_thin(self.host(), rng, density), self._ctx)
+        """CsrMatrix::thin (src/graph_csr.rs:225-247) on the device; `rng` advances like the reference's."""
+        v = self.view()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_thin(self._ctx.ptr, C.byref(v), C.byref(rng._s), float(density), C.byref(out)),
+                self._ctx.ptr)
+        return type(self)(out, self._ctx)
+
+    @classmethod
+    def from_coo_device(cls, n: int, rows, cols, vals, ctx: Context | None = None):
+        """CsrMatrix::from_coo (src/graph_csr.rs:83-129) on the device, from host triplet arrays."""
+        ctx = ctx or default_context()
+        r = np.ascontiguousarray(rows, np.uint32)
+        c = np.ascontiguousarray(cols, np.uint32)
+        v = np.ascontiguousarray(vals, _VDT[cls.DTYPE])
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_from_coo(ctx.ptr, n, len(r), r.ctypes.data, c.ctypes.data, v.ctypes.data, cls.DTYPE,
+                                          L.HOST, C.byref(out)), ctx.ptr)
+        return cls(out, ctx)
 
     # -- accessors ---------------------------------------------------------------------------------
     @property

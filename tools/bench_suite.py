@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=2.0, help="seconds of timed CPU calls per cell")
     ap.add_argument("--cpu-max-nnz", type=float, default=3e7, help="skip the CPU leg above this nnz(A)")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
-    ap.add_argument("--only", default="C1,C2,C3,C4,C5")
+    ap.add_argument("--only", default="GEN,C1,C2,C3,C4,C5")
     ap.add_argument("--rmat-scale", type=int, default=16)
     ap.add_argument("--rmat-deg", type=int, default=16)
     args = ap.parse_args()
@@ -121,6 +121,21 @@ def main():
     out = {"threads": args.threads, "cells": []}
     M = slat.CsrMatrix
 
+    if "GEN" in only:
+        # the reference's input generators (lattice + thin, seed [42;32]): host library vs device
+        for side in (30, 100):
+            t0 = time.perf_counter()
+            h = slat.torus_thinned(side, 3.0, slat.StdRng())
+            th = time.perf_counter() - t0
+            d = slat.torus_thinned_device(side, 3.0, slat.StdRng(), ctx)  # warm-up
+            t0 = time.perf_counter()
+            d = slat.torus_thinned_device(side, 3.0, slat.StdRng(), ctx)
+            td = time.perf_counter() - t0
+            same_arrays = bool(np.array_equal(d.host().col_idx, h.col_idx) and np.array_equal(d.host().row_ptr, h.row_ptr))
+            rec = {"cell": f"GEN torus{side} thinned 3 e/n", "n": h.n, "nnz_c": h.nnz, "host_ms": th * 1e3,
+                   "device_ms": td * 1e3, "identical": same_arrays}
+            print(json.dumps(rec), file=sys.stderr, flush=True)
+            out.setdefault("generators", []).append(rec)
     if only & {"C1", "C2"}:
         oA = O.torus_thinned(30, 3.0, O.Rng())
         dA = to_dev(oA, M, ctx)
@@ -168,6 +183,8 @@ def main():
         print(f"| {r['cell']} | {r['nnz_c']} | {r['gpu_ms']:.3f} | {r['gnnz_s']:.2f} | {f('numeric_hbm_frac', '%.3f')} "
               f"| {f('pipeline_hbm_frac', '%.3f')} | {f('cpu_ms', '%.2f')} | {f('cpu_gnnz_s', '%.3f')} "
               f"| {f('speedup', '%.0f')} | {r.get('bit_exact', r.get('within_rtol_1e-12', '-'))} |")
+    for g in out.get("generators", []):
+        print(f"\n{g['cell']}: host library {g['host_ms']:.1f} ms, device {g['device_ms']:.1f} ms, identical {g['identical']}")
 
 
 class _shape:
