@@ -92,6 +92,8 @@ slat_status slat_ctx_destroy(slat_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->cblk) (void)hipFreeAsync(ctx->cblk, ctx->cblk_stream);
+    (void)hipStreamSynchronize(ctx->stream);
     if (ctx->h_shards) (void)hipHostFree(ctx->h_shards);
     if (ctx->d_words) (void)hipFree(ctx->d_words);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
@@ -142,7 +144,18 @@ slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m) {
     if (!ctx || !m) return SLAT_EINVAL;
     (void)hipSetDevice(ctx->device);
     if (m->alloc == kAllocJoint) {
-        if (m->row_ptr) (void)hipFreeAsync(m->row_ptr, ctx->stream);
+        if (m->row_ptr) {
+            // keep the block for the next call's output (the larger of it and the cached one)
+            const size_t b = joint_bytes(m->n_rows, m->capacity, vsize(m->dtype));
+            if (b >= ctx->cblk_bytes) {
+                if (ctx->cblk) (void)hipFreeAsync(ctx->cblk, ctx->cblk_stream);
+                ctx->cblk = m->row_ptr;
+                ctx->cblk_bytes = b;
+                ctx->cblk_stream = ctx->stream;
+            } else {
+                (void)hipFreeAsync(m->row_ptr, ctx->stream);
+            }
+        }
     } else {
         if (m->row_ptr) (void)hipFreeAsync(m->row_ptr, ctx->stream);
         if (m->col_idx) (void)hipFreeAsync(m->col_idx, ctx->stream);
@@ -185,7 +198,7 @@ extern "C" slat_status slat_csr_create(slat_ctx *ctx, const slat_csr_view *src, 
     std::memset(out, 0, sizeof *out);
     const size_t vs = vsize(src->dtype);
     const hipMemcpyKind kind = src->residency == SLAT_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-    SLAT_HIP(ctx, alloc_joint(out, src->n_rows, src->nnz, vs, ctx->stream));
+    SLAT_HIP(ctx, alloc_joint(ctx, out, src->n_rows, src->nnz, vs, ctx->stream));
     if (src->n_rows)
         SLAT_HIP(ctx, hipMemcpyAsync(out->row_ptr, src->row_ptr, (src->n_rows + 1) * 8, kind, ctx->stream));
     else
@@ -474,7 +487,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     C->device = ctx->device;
     if (n == 0 || ncols == 0 || A->nnz == 0 || B->nnz == 0) {
         // empty product: all-zero row_ptr
-        SLAT_HIP(ctx, alloc_joint(C, n, 0, vs, s));
+        SLAT_HIP(ctx, alloc_joint(ctx, C, n, 0, vs, s));
         SLAT_HIP(ctx, hipMemsetAsync(C->row_ptr, 0, (n + 1) * 8, s));
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         return SLAT_OK;
@@ -609,7 +622,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
     if (!exact) {
         C->capacity = (uint64_t)std::max<unsigned __int128>(bound128, 1);
-        SLAT_HIP(ctx, alloc_joint(C, n, C->capacity, vs, s));
+        SLAT_HIP(ctx, alloc_joint(ctx, C, n, C->capacity, vs, s));
     } else {
         SLAT_HIP(ctx, hipMallocAsync((void **)&C->row_ptr, (n + 1) * 8, s));
         C->alloc = kAllocSeparate;

@@ -252,7 +252,7 @@ slat_status from_coo_dev(slat_ctx *ctx, uint64_t n, uint64_t nt, const uint32_t 
     out->device = ctx->device;
     const size_t vs = vsize(dt);
     if (nt == 0) {
-        SLAT_HIP(ctx, alloc_joint(out, n, 0, vs, s));
+        SLAT_HIP(ctx, alloc_joint(ctx, out, n, 0, vs, s));
         SLAT_HIP(ctx, hipMemsetAsync(out->row_ptr, 0, (n + 1) * 8, s));
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         return SLAT_OK;
@@ -295,7 +295,7 @@ slat_status from_coo_dev(slat_ctx *ctx, uint64_t n, uint64_t nt, const uint32_t 
     hipLaunchKernelGGL(k_coo_runs, g, b, 0, s, k2, i2, vals, dt, nt, head, upos, ukey, uval, keep);
     SLAT_HIP(ctx, hipGetLastError());
     if ((st = scan_total(ctx, keep, nu, fpos, &nnz))) return st;
-    SLAT_HIP(ctx, alloc_joint(out, n, nnz, vs, s));
+    SLAT_HIP(ctx, alloc_joint(ctx, out, n, nnz, vs, s));
     if (n) SLAT_HIP(ctx, hipMemsetAsync(rowcnt, 0, n * 8, s));
     if (nu) {
         hipLaunchKernelGGL(k_coo_emit, grid_for(ctx, nu), b, 0, s, ukey, uval, keep, fpos, nu, nnz, n, dt,

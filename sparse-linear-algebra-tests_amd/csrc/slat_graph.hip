@@ -116,7 +116,7 @@ extern "C" slat_status slat_csr_identity(slat_ctx *ctx, uint64_t n, int32_t dtyp
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
     std::memset(out, 0, sizeof *out);
     hipStream_t s = ctx->stream;
-    SLAT_HIP(ctx, alloc_joint(out, n, n, vsize(dtype), s));
+    SLAT_HIP(ctx, alloc_joint(ctx, out, n, n, vsize(dtype), s));
     const dim3 g = flat_grid(ctx, n + 1);
     if (dtype == SLAT_U32)
         hipLaunchKernelGGL(k_identity<uint32_t>, g, dim3(kBlock), 0, s, n, out->row_ptr, out->col_idx, (uint32_t *)out->values);
