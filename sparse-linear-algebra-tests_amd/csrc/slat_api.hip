@@ -1,7 +1,7 @@
 // slat_api.hip — C ABI (include/slat.h) over the gfx950 SpGEMM kernels.
 //
 // Orchestration of one C = A·B call on the context's stream:
-//   1. C.row_ptr and C.col/val allocated from the stream-ordered pool (hipMallocAsync). By
+//   1. C.row_ptr and C.col/val in one device block of the context's cache (slat_dev_alloc). By
 //      default C is sized by the exact upper bound nnz(A)·max_row_nnz(B) (clamped to rows·cols),
 //      so no host round trip is needed between the symbolic and numeric passes; the capacity is
 //      recorded in slat_csr.capacity. SLAT_FLAG_EXACT_ALLOC (or a bound above the memory budget)
@@ -62,12 +62,6 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         return SLAT_EHIP;
     }
     ctx->stream = ctx->own_stream;
-    // keep freed pool memory cached: C arrays are allocated every call
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-        uint64_t thr = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    }
     if (hipHostMalloc((void **)&ctx->h_shards, sizeof(unsigned long long) * kShards * kShardStride) != hipSuccess) {
         (void)hipStreamDestroy(ctx->own_stream);
         delete ctx;
@@ -92,11 +86,10 @@ slat_status slat_ctx_destroy(slat_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
-    if (ctx->cblk) (void)hipFreeAsync(ctx->cblk, ctx->cblk_stream);
-    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_status) slat_dev_free(ctx, ctx->d_status, ctx->stream);
+    slat_dev_trim(ctx);
     if (ctx->h_shards) (void)hipHostFree(ctx->h_shards);
     if (ctx->d_words) (void)hipFree(ctx->d_words);
-    if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->h_out) (void)hipHostFree(ctx->h_out);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->own_stream);
@@ -144,22 +137,11 @@ slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m) {
     if (!ctx || !m) return SLAT_EINVAL;
     (void)hipSetDevice(ctx->device);
     if (m->alloc == kAllocJoint) {
-        if (m->row_ptr) {
-            // keep the block for the next call's output (the larger of it and the cached one)
-            const size_t b = joint_bytes(m->n_rows, m->capacity, vsize(m->dtype));
-            if (b >= ctx->cblk_bytes) {
-                if (ctx->cblk) (void)hipFreeAsync(ctx->cblk, ctx->cblk_stream);
-                ctx->cblk = m->row_ptr;
-                ctx->cblk_bytes = b;
-                ctx->cblk_stream = ctx->stream;
-            } else {
-                (void)hipFreeAsync(m->row_ptr, ctx->stream);
-            }
-        }
+        if (m->row_ptr) slat_dev_free(ctx, m->row_ptr, ctx->stream);
     } else {
-        if (m->row_ptr) (void)hipFreeAsync(m->row_ptr, ctx->stream);
-        if (m->col_idx) (void)hipFreeAsync(m->col_idx, ctx->stream);
-        if (m->values) (void)hipFreeAsync(m->values, ctx->stream);
+        if (m->row_ptr) slat_dev_free(ctx, m->row_ptr, ctx->stream);
+        if (m->col_idx) slat_dev_free(ctx, m->col_idx, ctx->stream);
+        if (m->values) slat_dev_free(ctx, m->values, ctx->stream);
     }
     std::memset(m, 0, sizeof *m);
     return SLAT_OK;
@@ -168,6 +150,67 @@ slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m) {
 }  // extern "C"
 
 // ---------------------------------------------------------------------------------------------
+// Device blocks (slat_internal.hpp). Sizes round to 4 KiB (to 2 MiB above 1 MiB) so repeated calls
+// of similar size find their block; a cached block serves a request of at least a quarter of it.
+// Measured reason for not using hipMallocAsync (ROCm 7.2 image): after a thin call freed pool
+// blocks, a 324 MB lattice allocation read back zeros for a 26 MiB range of k_lattice's row writes
+// (the column writes of the same threads, in another range, were intact); with the default release
+// threshold a later scan spun forever on status words it had written. hipMalloc: correct.
+static size_t round_block(size_t b) {
+    const size_t g = b > ((size_t)1 << 20) ? ((size_t)2 << 20) : 4096;
+    return (std::max<size_t>(b, 1) + g - 1) / g * g;
+}
+static constexpr size_t kCacheMax = (size_t)32 << 30;  // cached bytes kept at most (of 288 GB)
+
+hipError_t slat_dev_alloc(slat_ctx *ctx, void **p, size_t bytes, hipStream_t s) {
+    const size_t r = round_block(bytes);
+    size_t best = SIZE_MAX;
+    for (size_t i = 0; i < ctx->cache.size(); ++i) {
+        const auto &c = ctx->cache[i];
+        if (c.s == s && c.bytes >= r && c.bytes / 4 <= r && (best == SIZE_MAX || c.bytes < ctx->cache[best].bytes)) best = i;
+    }
+    if (best != SIZE_MAX) {
+        *p = ctx->cache[best].p;
+        ctx->live[*p] = ctx->cache[best].bytes;
+        ctx->cache_bytes -= ctx->cache[best].bytes;
+        ctx->cache.erase(ctx->cache.begin() + (std::ptrdiff_t)best);
+        return hipSuccess;
+    }
+    hipError_t e = hipMalloc(p, r);
+    if (e == hipErrorOutOfMemory && !ctx->cache.empty()) {
+        (void)hipGetLastError();
+        slat_dev_trim(ctx);
+        e = hipMalloc(p, r);
+    }
+    if (e == hipSuccess) ctx->live[*p] = r;
+    return e;
+}
+
+void slat_dev_free(slat_ctx *ctx, void *p, hipStream_t s) {
+    auto it = ctx->live.find(p);
+    if (it == ctx->live.end()) return;  // not ours (or freed already)
+    const size_t b = it->second;
+    ctx->live.erase(it);
+    ctx->cache.push_back({p, b, s});
+    ctx->cache_bytes += b;
+    if (ctx->cache_bytes > kCacheMax) {
+        (void)hipDeviceSynchronize();  // the evicted blocks may still be read by queued work
+        while (ctx->cache_bytes > kCacheMax / 2 && !ctx->cache.empty()) {
+            ctx->cache_bytes -= ctx->cache.front().bytes;
+            (void)hipFree(ctx->cache.front().p);
+            ctx->cache.erase(ctx->cache.begin());
+        }
+    }
+}
+
+void slat_dev_trim(slat_ctx *ctx) {
+    if (ctx->cache.empty()) return;
+    (void)hipDeviceSynchronize();
+    for (auto &c : ctx->cache) (void)hipFree(c.p);
+    ctx->cache.clear();
+    ctx->cache_bytes = 0;
+}
+
 slat_status slat_ensure_ws(slat_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->ws_bytes) return SLAT_OK;
     SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -393,9 +436,10 @@ static hipError_t launch_compact(dim3 grid, hipStream_t s, const uint64_t *orp, 
 slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s) {
     const uint64_t tiles = std::max<uint64_t>((n + kScanTile - 1) / kScanTile, 1);
     if (tiles > ctx->status_cap) {
-        if (ctx->d_status) SLAT_HIP(ctx, hipFreeAsync(ctx->d_status, s));
+        if (ctx->d_status) slat_dev_free(ctx, ctx->d_status, s);
+        ctx->d_status = nullptr;
         const uint64_t cap = std::max<uint64_t>(tiles, 1024);
-        SLAT_HIP(ctx, hipMallocAsync((void **)&ctx->d_status, cap * 8, s));
+        SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&ctx->d_status, cap * 8, s));
         SLAT_HIP(ctx, hipMemsetAsync(ctx->d_status, 0, cap * 8, s));
         ctx->status_cap = cap;
     }
@@ -624,7 +668,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         C->capacity = (uint64_t)std::max<unsigned __int128>(bound128, 1);
         SLAT_HIP(ctx, alloc_joint(ctx, C, n, C->capacity, vs, s));
     } else {
-        SLAT_HIP(ctx, hipMallocAsync((void **)&C->row_ptr, (n + 1) * 8, s));
+        SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&C->row_ptr, (n + 1) * 8, s));
         C->alloc = kAllocSeparate;
     }
     a.c_rp = C->row_ptr;
@@ -705,8 +749,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         const uint64_t total = ctx->h_out[0];
         C->capacity = std::max<uint64_t>(total, 1);
-        if (hipMallocAsync((void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
-            hipMallocAsync(&C->values, C->capacity * vs, s) != hipSuccess) {
+        if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
+            slat_dev_alloc(ctx, &C->values, C->capacity * vs, s) != hipSuccess) {
             slat_csr_free(ctx, C);
             return fail(ctx, SLAT_EOOM, "C allocation failed");
         }
@@ -770,15 +814,15 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (drops) {
         // exact zeros were dropped: rebuild row_ptr from the per-row actual counts and move rows
         uint64_t *nrp = nullptr;
-        SLAT_HIP(ctx, hipMallocAsync((void **)&nrp, (n + 1) * 8, s));
+        SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&nrp, (n + 1) * 8, s));
         if ((st = slat_launch_scan(ctx, a.counts, n, nrp, s))) return st;
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         const uint64_t total = ctx->h_out[0];
         maxrow = ctx->h_out[1];
         uint32_t *ncol = nullptr;
         void *nval = nullptr;
-        SLAT_HIP(ctx, hipMallocAsync((void **)&ncol, std::max<uint64_t>(total, 1) * 4, s));
-        SLAT_HIP(ctx, hipMallocAsync(&nval, std::max<uint64_t>(total, 1) * vs, s));
+        SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&ncol, std::max<uint64_t>(total, 1) * 4, s));
+        SLAT_HIP(ctx, slat_dev_alloc(ctx, &nval, std::max<uint64_t>(total, 1) * vs, s));
         if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
         if (dt == SLAT_U32)
             e = launch_compact<SemU32>(sym_grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);

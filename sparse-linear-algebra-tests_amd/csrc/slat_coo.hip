@@ -228,8 +228,9 @@ __global__ void k_narrow_u32(const uint64_t *in, uint64_t n, uint32_t *out) {
 struct Buf {
     slat_ctx *ctx;
     void *p = nullptr;
+    hipError_t alloc(size_t bytes) { return slat_dev_alloc(ctx, &p, bytes, ctx->stream); }
     ~Buf() {
-        if (p) (void)hipFreeAsync(p, ctx->stream);
+        if (p) slat_dev_free(ctx, p, ctx->stream);
     }
 };
 
@@ -274,7 +275,7 @@ slat_status from_coo_dev(slat_ctx *ctx, uint64_t n, uint64_t nt, const uint32_t 
                  o_st = o_rc + up(n * 8), total_b = o_st + up(sort_b);
     if (nt > 0xFFFFFFFFull) return fail(ctx, SLAT_ENOTSUP, "more than 2^32 triplets");
     Buf scratch{ctx};
-    if (hipMallocAsync(&scratch.p, total_b, s) != hipSuccess) return fail(ctx, SLAT_EOOM, "from_coo scratch");
+    if (scratch.alloc(total_b) != hipSuccess) return fail(ctx, SLAT_EOOM, "from_coo scratch");
     uint8_t *w = (uint8_t *)scratch.p;
     uint64_t *k1 = (uint64_t *)w, *k2 = (uint64_t *)(w + o_k2);
     uint32_t *i1 = (uint32_t *)(w + o_i1), *i2 = (uint32_t *)(w + o_i2);
@@ -324,7 +325,7 @@ extern "C" slat_status slat_csr_from_coo(slat_ctx *ctx, uint64_t n, uint64_t ntr
     Buf stage{ctx};
     const size_t vs = vsize(dtype);
     const size_t bytes = ntrip * (8 + vs) + 64;
-    if (hipMallocAsync(&stage.p, bytes, ctx->stream) != hipSuccess) return fail(ctx, SLAT_EOOM, "from_coo staging");
+    if (stage.alloc(bytes) != hipSuccess) return fail(ctx, SLAT_EOOM, "from_coo staging");
     uint8_t *d = (uint8_t *)stage.p;
     if (ntrip) {
         SLAT_HIP(ctx, hipMemcpyAsync(d, rows, ntrip * 4, hipMemcpyHostToDevice, ctx->stream));
@@ -352,7 +353,7 @@ extern "C" slat_status slat_csr_lattice(slat_ctx *ctx, const uint64_t *dims, int
     for (int d = ndim - 2; d >= 0; --d) L.strides[d] = L.strides[d + 1] * dims[d + 1];
     const uint64_t nt = total * nnb;
     Buf trip{ctx};
-    if (hipMallocAsync(&trip.p, nt * 12 + 64, ctx->stream) != hipSuccess) return fail(ctx, SLAT_EOOM, "lattice triplets");
+    if (trip.alloc(nt * 12 + 64) != hipSuccess) return fail(ctx, SLAT_EOOM, "lattice triplets");
     uint32_t *rows = (uint32_t *)trip.p, *cols = rows + nt, *vals = cols + nt;
     hipLaunchKernelGGL(k_lattice, grid_for(ctx, nt), dim3(kB), 0, ctx->stream, L, torus, total, nnb, rows, cols);
     SLAT_HIP(ctx, hipGetLastError());
@@ -376,7 +377,7 @@ extern "C" slat_status slat_csr_thin(slat_ctx *ctx, const slat_csr_view *m, slat
     const size_t o_dp = up(nnz * 8), o_em = o_dp + up((nnz + 1) * 8), o_ep = o_em + up(nnz * 8),
                  o_tr = o_ep + up((nnz + 1) * 8), o_tc = o_tr + up(2 * nnz * 4), o_tv = o_tc + up(2 * nnz * 4),
                  o_tn = o_tv + up(2 * nnz * 8), total_b = o_tn + up(2 * nnz * 4) + 256;
-    if (hipMallocAsync(&scratch.p, total_b, s) != hipSuccess) return fail(ctx, SLAT_EOOM, "thin scratch");
+    if (scratch.alloc(total_b) != hipSuccess) return fail(ctx, SLAT_EOOM, "thin scratch");
     uint8_t *w = (uint8_t *)scratch.p;
     uint64_t *need = (uint64_t *)w, *dpos = (uint64_t *)(w + o_dp), *emit = (uint64_t *)(w + o_em),
              *epos = (uint64_t *)(w + o_ep), *tval = (uint64_t *)(w + o_tv);

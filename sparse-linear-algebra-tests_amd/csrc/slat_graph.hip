@@ -45,7 +45,7 @@ slat_status add_typed(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view
     slat_status st = slat_ensure_ws(ctx, std::max<uint64_t>(n, 1) * 8);
     if (st) return st;
     uint64_t *counts = (uint64_t *)ctx->ws;
-    SLAT_HIP(ctx, hipMallocAsync((void **)&C->row_ptr, (n + 1) * 8, s));
+    SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&C->row_ptr, (n + 1) * 8, s));
     C->alloc = kAllocSeparate;
     const dim3 g = wave_grid(ctx, n);
     hipLaunchKernelGGL((k_add<S, true>), g, dim3(kBlock), 0, s, A->row_ptr, A->col_idx, (const S *)A->values,
@@ -58,8 +58,8 @@ slat_status add_typed(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view
     C->nnz = nnz;
     C->capacity = std::max<uint64_t>(nnz, 1);
     C->max_row_nnz = ctx->h_out[1];
-    SLAT_HIP(ctx, hipMallocAsync((void **)&C->col_idx, C->capacity * 4, s));
-    SLAT_HIP(ctx, hipMallocAsync(&C->values, C->capacity * sizeof(S), s));
+    SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s));
+    SLAT_HIP(ctx, slat_dev_alloc(ctx, &C->values, C->capacity * sizeof(S), s));
     hipLaunchKernelGGL((k_add<S, false>), g, dim3(kBlock), 0, s, A->row_ptr, A->col_idx, (const S *)A->values,
                        B->row_ptr, B->col_idx, (const S *)B->values, n, nullptr, C->row_ptr, C->col_idx,
                        (S *)C->values);

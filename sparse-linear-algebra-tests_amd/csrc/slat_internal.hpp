@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <cstdint>
 #include <string>
+#include <unordered_map>
+#include <vector>
 
 #include "slat.h"
 
@@ -32,10 +34,15 @@ struct slat_ctx {
     size_t free_b = 0;                       // cached hipMemGetInfo free bytes
     uint32_t free_age = 0;
     hipEvent_t ev[6] = {};
-    // one freed joint block kept for the next output (saves a pool allocate + free per call)
-    void *cblk = nullptr;
-    size_t cblk_bytes = 0;
-    hipStream_t cblk_stream = nullptr;
+    // device blocks: hipMalloc'd, cached after free and reused in stream order (slat_dev_alloc)
+    struct Block {
+        void *p;
+        size_t bytes;
+        hipStream_t s;
+    };
+    std::vector<Block> cache;                  // freed blocks, oldest first
+    size_t cache_bytes = 0;
+    std::unordered_map<void *, size_t> live;   // allocated block -> its size
     slat_stats stats = {};
 };
 
@@ -55,28 +62,28 @@ static inline slat_status fail(slat_ctx *ctx, slat_status s, const std::string &
 
 static inline size_t vsize(int32_t dtype) { return dtype == SLAT_U32 ? 4 : 8; }
 
-// C arrays in one stream-ordered pool block (one malloc, one free per matrix):
+// C arrays in one device block (one allocation, one free per matrix):
 // row_ptr | col_idx | values, each 256-byte aligned. alloc = 1 marks the layout for slat_csr_free.
 enum { kAllocSeparate = 0, kAllocJoint = 1 };
 static inline size_t joint_bytes(uint64_t nrows, uint64_t cap, size_t vs) {
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     return up((nrows + 1) * 8) + up(std::max<uint64_t>(cap, 1) * 4) + std::max<uint64_t>(cap, 1) * vs;
 }
-// One block of the layout above: the context's cached block when it is large enough and from the
-// same stream (a freed C of a previous call, see slat_csr_free), else a stream-ordered allocation.
+// Device memory of the library (C arrays, scan status, constructor scratch): blocks from hipMalloc,
+// kept by the context after slat_dev_free and handed out again on the same stream (stream order
+// makes the reuse safe without a sync). Not hipMallocAsync: on this image its pool lost kernel
+// writes to part of a freshly grown block ("Device memory").
+hipError_t slat_dev_alloc(slat_ctx *ctx, void **p, size_t bytes, hipStream_t s);
+void slat_dev_free(slat_ctx *ctx, void *p, hipStream_t s);
+void slat_dev_trim(slat_ctx *ctx);  // device sync, then every cached block back to the driver
+
+// One block of the layout above.
 static inline hipError_t alloc_joint(slat_ctx *ctx, slat_csr *m, uint64_t nrows, uint64_t cap, size_t vs, hipStream_t s) {
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t rp_b = up((nrows + 1) * 8), col_b = up(std::max<uint64_t>(cap, 1) * 4);
-    const size_t bytes = joint_bytes(nrows, cap, vs);
     uint8_t *base = nullptr;
-    if (ctx->cblk && ctx->cblk_stream == s && ctx->cblk_bytes >= bytes && ctx->cblk_bytes / 4 <= bytes) {
-        base = (uint8_t *)ctx->cblk;  // reuse: a block at most 4x the request
-        ctx->cblk = nullptr;
-        ctx->cblk_bytes = 0;
-    } else {
-        const hipError_t e = hipMallocAsync((void **)&base, bytes, s);
-        if (e != hipSuccess) return e;
-    }
+    const hipError_t e = slat_dev_alloc(ctx, (void **)&base, joint_bytes(nrows, cap, vs), s);
+    if (e != hipSuccess) return e;
     m->row_ptr = (uint64_t *)base;
     m->col_idx = (uint32_t *)(base + rp_b);
     m->values = base + rp_b + col_b;

@@ -85,3 +85,18 @@ def test_torus100_device_generator_golden(ctx, golden):
     a = slat.torus_thinned_device(100, 3.0, slat.StdRng(), ctx)
     h = a.host()
     assert_digest(digest(h.row_ptr, h.col_idx, h.values), golden["torus100_powers"][0], "100^3 A (device)")
+
+
+def test_generators_small_then_large_same_context(golden):
+    # the sequence that exposed lost writes in the stream-ordered pool (DESIGN.md "Device memory"):
+    # a 30^3 generation frees scratch, then the 100^3 lattice grows past it, on one fresh context
+    c = slat.Context(0)
+    for rep in range(2):
+        a = slat.torus_thinned_device(30, 3.0, slat.StdRng(), c)
+        h = a.host()
+        assert_digest(digest(h.row_ptr, h.col_idx, h.values), golden["torus30_powers"][0], f"30^3 A rep {rep}")
+        del a
+        b = slat.torus_thinned_device(100, 3.0, slat.StdRng(), c)
+        h = b.host()
+        assert_digest(digest(h.row_ptr, h.col_idx, h.values), golden["torus100_powers"][0], f"100^3 A rep {rep}")
+        del b
