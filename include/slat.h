@@ -17,6 +17,11 @@
  *   CsrMatrix::reachability_sum    src/graph_csr.rs:545-559  slat_reachability_sum
  *   CsrMatrix::power_until_stable  src/graph_csr.rs:562-577  slat_power_until_stable
  *   CsrMatrix::connected_components src/graph_csr.rs:580-603 slat_connected_components
+ *   CsrMatrix::from_edges{,_undirected} src/graph_csr.rs:132-147 slat_csr_from_edges
+ *   CsrMatrix::rcm          src/graph_csr.rs:663-722         slat_rcm_order + slat_csr_permute
+ *   CsrMatrix::permute / unpermute src/graph_csr.rs:726-799  slat_csr_permute
+ *   CsrMatrix::bandwidth_stats src/graph_csr.rs:802-818      slat_bandwidth_stats
+ *   load_edges (tests)      src/graph_csr.rs:1209-1224       slat_load_edges
  *   assert_eq!(self.n, other.n) panics (graph_csr.rs:307,351)  -> SLAT_EDIM
  *
  * Conventions:
@@ -204,6 +209,28 @@ slat_status slat_csr_lattice(slat_ctx *ctx, const uint64_t *dims, int ndim, int 
  * *rng ends where the reference's generator would. */
 slat_status slat_csr_thin(slat_ctx *ctx, const slat_csr_view *m, slat_rng *rng, double density,
                           slat_csr *out);
+
+/* --- the real-graph path -------------------------------------------- */
+/* load_edges (src/graph_csr.rs:1209-1224): "<a> <b>" per non-empty line (further tokens ignored);
+ * n = max id + 1; *src, *dst are malloc'd host arrays of *n_edges ids (free: slat_edges_free).
+ * Unreadable file or malformed line -> SLAT_EINVAL (the reference panics). */
+slat_status slat_load_edges(const char *path, uint64_t *n, uint64_t *n_edges, uint32_t **src, uint32_t **dst);
+void slat_edges_free(uint32_t *src, uint32_t *dst);
+/* CsrMatrix::from_edges (undirected = 0) / from_edges_undirected (= 1), src/graph_csr.rs:132-147:
+ * u32 value 1 per edge (and per mirrored edge r != c), then from_coo (duplicates summed). */
+slat_status slat_csr_from_edges(slat_ctx *ctx, uint64_t n, uint64_t n_edges, const uint32_t *src,
+                                const uint32_t *dst, int32_t undirected, int32_t residency, slat_csr *out);
+/* The order CsrMatrix::rcm (src/graph_csr.rs:663-722) permutes by, perm[new] = old, into the host
+ * array perm[n]. Degree ties keep column order (the reference's unstable sort leaves them open).
+ * An order that is not a permutation (possible on directed graphs) -> SLAT_EINVAL. */
+slat_status slat_rcm_order(slat_ctx *ctx, const slat_csr_view *m, uint32_t *perm);
+/* CsrMatrix::permute (src/graph_csr.rs:726-783), perm[new] = old (device or host per
+ * perm_residency); out = rows and columns renumbered, columns sorted, explicit zeros kept.
+ * unpermute is permute by the inverse. perm not a permutation of 0..n -> SLAT_EINVAL. */
+slat_status slat_csr_permute(slat_ctx *ctx, const slat_csr_view *m, const uint32_t *perm, int32_t perm_residency,
+                             slat_csr *out);
+/* CsrMatrix::bandwidth_stats (src/graph_csr.rs:802-818): max |r-c| and mean |r-c| over entries. */
+slat_status slat_bandwidth_stats(slat_ctx *ctx, const slat_csr_view *m, uint64_t *max_bw, double *avg_bw);
 
 
 #ifdef __cplusplus

@@ -7,6 +7,7 @@
 
 #include <pthread.h>
 #include <stdatomic.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -777,5 +778,162 @@ int orc_connected_components(const orc_csr *a, uint64_t *component) {
             if (has_entry(&closure, i, (uint32_t)j) && has_entry(&closure, j, (uint32_t)i)) component[j] = cid;
     }
     orc_csr_free(&closure);
+    return 0;
+}
+
+/* ---- CsrMatrix::rcm order (src/graph_csr.rs:663-722) ------------------------------------------
+ * For every unvisited seed in id order: a plain BFS (neighbours in column order) whose last popped
+ * node is the start; then a BFS from the start that visits each node's unvisited neighbours by
+ * ascending degree (ties in column order); the concatenated visit order, reversed. */
+static uint64_t deg_of(const orc_csr *a, uint64_t v) { return a->row_ptr[v + 1] - a->row_ptr[v]; }
+
+int orc_rcm_order(const orc_csr *a, uint32_t *perm) {
+    const uint64_t n = a->n;
+    uint8_t *visited = calloc(n ? n : 1, 1);
+    uint64_t *stamp = calloc(n ? n : 1, 8); /* vis2 of seed s: stamp == s + 1 */
+    uint64_t *queue = malloc((n + 2) * 8);
+    uint64_t *order = malloc((2 * n + 1) * 8);
+    uint64_t *nbrs = malloc((n ? n : 1) * 8);
+    uint64_t olen = 0;
+    int rc = 0;
+    for (uint64_t seed = 0; seed < n; ++seed) {
+        if (visited[seed]) continue;
+        uint64_t qh = 0, qt = 0, last = seed;
+        stamp[seed] = seed + 1;
+        queue[qt++] = seed;
+        while (qh < qt) {
+            const uint64_t u = queue[qh++];
+            last = u;
+            for (uint64_t i = a->row_ptr[u]; i < a->row_ptr[u + 1]; ++i) {
+                const uint64_t v = a->col[i];
+                if (stamp[v] != seed + 1) {
+                    stamp[v] = seed + 1;
+                    queue[qt++] = v;
+                }
+            }
+        }
+        const uint64_t start = last;
+        qh = qt = 0;
+        queue[qt++] = start;
+        visited[start] = 1;
+        while (qh < qt) {
+            const uint64_t u = queue[qh++];
+            if (olen >= 2 * n) { rc = -1; goto done; }
+            order[olen++] = u;
+            uint64_t k = 0;
+            for (uint64_t i = a->row_ptr[u]; i < a->row_ptr[u + 1]; ++i)
+                if (!visited[a->col[i]]) nbrs[k++] = a->col[i];
+            /* stable insertion sort by degree (k is a row length) */
+            for (uint64_t x = 1; x < k; ++x) {
+                const uint64_t v = nbrs[x], dv = deg_of(a, v);
+                uint64_t y = x;
+                while (y > 0 && deg_of(a, nbrs[y - 1]) > dv) { nbrs[y] = nbrs[y - 1]; --y; }
+                nbrs[y] = v;
+            }
+            for (uint64_t x = 0; x < k; ++x)
+                if (!visited[nbrs[x]]) {
+                    visited[nbrs[x]] = 1;
+                    if (qt > n) { rc = -1; goto done; }
+                    queue[qt++] = nbrs[x];
+                }
+        }
+    }
+    if (olen != n) { rc = -1; goto done; }
+    for (uint64_t i = 0; i < n; ++i) perm[i] = (uint32_t)order[n - 1 - i];
+done:
+    free(visited); free(stamp); free(queue); free(order); free(nbrs);
+    return rc;
+}
+
+/* CsrMatrix::permute (src/graph_csr.rs:726-783): new row inv[r] holds row r's entries with
+ * columns inv[c], sorted by column (a permutation has no duplicate columns, so order is unique) */
+int orc_permute(const orc_csr *a, const uint32_t *perm, orc_csr *out) {
+    const uint64_t n = a->n, nnz = a->nnz;
+    const size_t vs = a->dtype == ORC_U32 ? 4 : 8;
+    uint32_t *inv = malloc((n ? n : 1) * 4);
+    for (uint64_t i = 0; i < n; ++i) inv[perm[i]] = (uint32_t)i;
+    out->n = n;
+    out->nnz = nnz;
+    out->dtype = a->dtype;
+    out->row_ptr = calloc(n + 1, 8);
+    out->col = malloc((nnz ? nnz : 1) * 4);
+    out->val = malloc((nnz ? nnz : 1) * vs);
+    for (uint64_t r = 0; r < n; ++r) out->row_ptr[inv[r] + 1] = a->row_ptr[r + 1] - a->row_ptr[r];
+    for (uint64_t i = 1; i <= n; ++i) out->row_ptr[i] += out->row_ptr[i - 1];
+    for (uint64_t r = 0; r < n; ++r) {
+        const uint64_t nr = inv[r], s = a->row_ptr[r], e = a->row_ptr[r + 1];
+        uint64_t pos = out->row_ptr[nr];
+        for (uint64_t i = s; i < e; ++i, ++pos) {
+            /* insertion into the sorted prefix of the new row */
+            const uint32_t c = inv[a->col[i]];
+            uint64_t y = pos;
+            while (y > out->row_ptr[nr] && out->col[y - 1] > c) {
+                out->col[y] = out->col[y - 1];
+                memcpy((char *)out->val + y * vs, (char *)out->val + (y - 1) * vs, vs);
+                --y;
+            }
+            out->col[y] = c;
+            memcpy((char *)out->val + y * vs, (const char *)a->val + i * vs, vs);
+        }
+    }
+    free(inv);
+    return 0;
+}
+
+void orc_bandwidth_stats(const orc_csr *a, uint64_t *max_bw, double *avg_bw) {
+    uint64_t mx = 0, sum = 0;
+    for (uint64_t r = 0; r < a->n; ++r)
+        for (uint64_t i = a->row_ptr[r]; i < a->row_ptr[r + 1]; ++i) {
+            const uint64_t c = a->col[i], d = r > c ? r - c : c - r;
+            if (d > mx) mx = d;
+            sum += d;
+        }
+    *max_bw = mx;
+    *avg_bw = (double)sum / (double)(a->nnz ? a->nnz : 1);
+}
+
+/* load_edges (src/graph_csr.rs:1209-1224): lines trimmed, empty ones skipped, the first two
+ * whitespace-separated tokens parsed as u32 (further tokens ignored) */
+int orc_load_edges(const char *path, uint64_t *n, uint64_t *n_edges, uint32_t **src, uint32_t **dst) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return -1;
+    uint64_t cap = 1024, m = 0;
+    uint32_t *s = malloc(cap * 4), *d = malloc(cap * 4), max_id = 0;
+    char line[4096];
+    int rc = 0;
+    while (fgets(line, sizeof line, f)) {
+        char *p = line;
+        uint64_t v[2];
+        int got = 0;
+        while (got < 2) {
+            while (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\n' || *p == '\f' || *p == '\v') ++p;
+            if (!*p) break;
+            if (*p == '+') ++p; /* str::parse::<u32> takes a leading '+' */
+            if (*p < '0' || *p > '9') { rc = -1; goto done; }
+            uint64_t x = 0;
+            while (*p >= '0' && *p <= '9') {
+                x = x * 10 + (uint64_t)(*p++ - '0');
+                if (x > 0xFFFFFFFFull) { rc = -1; goto done; }
+            }
+            if (*p && *p != ' ' && *p != '\t' && *p != '\r' && *p != '\n' && *p != '\f' && *p != '\v') { rc = -1; goto done; }
+            v[got++] = x;
+        }
+        if (got == 0) continue;
+        if (got == 1) { rc = -1; goto done; }
+        if (m == cap) { cap *= 2; s = realloc(s, cap * 4); d = realloc(d, cap * 4); }
+        s[m] = (uint32_t)v[0];
+        d[m] = (uint32_t)v[1];
+        if (s[m] > max_id) max_id = s[m];
+        if (d[m] > max_id) max_id = d[m];
+        ++m;
+    }
+    if (max_id == 0xFFFFFFFFu) rc = -1;
+done:
+    fclose(f);
+    if (rc) { free(s); free(d); return rc; }
+    *n = (uint64_t)max_id + 1;
+    *n_edges = m;
+    *src = s;
+    *dst = d;
     return 0;
 }

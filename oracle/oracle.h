@@ -21,6 +21,12 @@
  *   orc_reachability_sum      CsrMatrix::reachability_sum      src/graph_csr.rs:545-559
  *   orc_power_until_stable    CsrMatrix::power_until_stable    src/graph_csr.rs:562-577
  *   orc_connected_components  CsrMatrix::connected_components  src/graph_csr.rs:580-603
+ *   orc_rcm_order    CsrMatrix::rcm              src/graph_csr.rs:663-722 (the order it permutes by;
+ *                    ties of the degree sort in column order: the reference's sort_unstable leaves
+ *                    them unspecified, so tie order is unpinned)
+ *   orc_permute      CsrMatrix::permute          src/graph_csr.rs:726-783 (perm[new] = old)
+ *   orc_bandwidth_stats CsrMatrix::bandwidth_stats src/graph_csr.rs:802-818
+ *   orc_load_edges   load_edges                  src/graph_csr.rs:1209-1224
  *
  * Parity pin: see tests/golden/ (nnz sequence that rounds to README.md:41-46, SHA-256 of the
  * arrays computed independently by tests/golden/make_golden.py with numpy+scipy).
@@ -71,6 +77,13 @@ int orc_identity(uint64_t n, int dtype, orc_csr *out);
 int orc_power_until_stable(const orc_csr *a, uint64_t *k, orc_csr *out);
 int orc_reachability_sum(const orc_csr *a, uint64_t *k, orc_csr *out);
 int orc_connected_components(const orc_csr *a, uint64_t *component);
+/* perm (n entries, malloc'd) = the order rcm() permutes by; -1 if that order is not a permutation
+ * (a directed graph whose peripheral BFS re-enters a finished component: the reference panics) */
+int orc_rcm_order(const orc_csr *a, uint32_t *perm);
+int orc_permute(const orc_csr *a, const uint32_t *perm, orc_csr *out);
+void orc_bandwidth_stats(const orc_csr *a, uint64_t *max_bw, double *avg_bw);
+/* "<a> <b>" per non-empty line; n = max id + 1; src and dst arrays malloc-ed. -1 on a malformed line. */
+int orc_load_edges(const char *path, uint64_t *n, uint64_t *n_edges, uint32_t **src, uint32_t **dst);
 
 #ifdef __cplusplus
 }

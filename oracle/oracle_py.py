@@ -66,6 +66,10 @@ def lib():
         L.orc_power_until_stable.argtypes = [P(_Csr), P(C.c_uint64), P(_Csr)]
         L.orc_reachability_sum.argtypes = [P(_Csr), P(C.c_uint64), P(_Csr)]
         L.orc_connected_components.argtypes = [P(_Csr), C.c_void_p]
+        L.orc_rcm_order.argtypes = [P(_Csr), C.c_void_p]
+        L.orc_permute.argtypes = [P(_Csr), C.c_void_p, P(_Csr)]
+        L.orc_bandwidth_stats.argtypes = [P(_Csr), P(C.c_uint64), P(C.c_double)]
+        L.orc_load_edges.argtypes = [C.c_char_p, P(C.c_uint64), P(C.c_uint64), P(C.c_void_p), P(C.c_void_p)]
         _lib = L
     return _lib
 
@@ -213,6 +217,55 @@ def connected_components(a: Csr) -> np.ndarray:
     if rc != 0:
         raise RuntimeError(f"oracle call failed rc={rc}")
     return out[:a.n]
+
+
+def rcm_order(a: Csr) -> np.ndarray:
+    """The order CsrMatrix::rcm (src/graph_csr.rs:663-722) permutes by (perm[new] = old)."""
+    out = np.empty(max(a.n, 1), np.uint32)
+    if lib().orc_rcm_order(C.byref(a._raw), out.ctypes.data) != 0:
+        raise ValueError("rcm order is not a permutation (the reference panics in permute)")
+    return out[:a.n]
+
+
+def permute(a: Csr, perm) -> Csr:
+    """CsrMatrix::permute (src/graph_csr.rs:726-783), perm[new] = old."""
+    p = np.ascontiguousarray(perm, np.uint32)
+    assert len(p) == a.n
+    return _new(lib().orc_permute, C.byref(a._raw), p.ctypes.data)
+
+
+def bandwidth_stats(a: Csr):
+    """CsrMatrix::bandwidth_stats (src/graph_csr.rs:802-818) -> (max |r-c|, mean |r-c|)."""
+    mx, avg = C.c_uint64(), C.c_double()
+    lib().orc_bandwidth_stats(C.byref(a._raw), C.byref(mx), C.byref(avg))
+    return int(mx.value), float(avg.value)
+
+
+def load_edges(path: str):
+    """load_edges (src/graph_csr.rs:1209-1224) -> (n, src u32[], dst u32[])."""
+    n, m, s, d = C.c_uint64(), C.c_uint64(), C.c_void_p(), C.c_void_p()
+    if lib().orc_load_edges(str(path).encode(), C.byref(n), C.byref(m), C.byref(s), C.byref(d)) != 0:
+        raise ValueError(f"cannot parse {path}")
+    k = int(m.value)
+    src = np.ctypeslib.as_array(C.cast(s, C.POINTER(C.c_uint32)), (max(k, 1),))[:k].copy()
+    dst = np.ctypeslib.as_array(C.cast(d, C.POINTER(C.c_uint32)), (max(k, 1),))[:k].copy()
+    libc = C.CDLL(None)
+    libc.free(s)
+    libc.free(d)
+    return int(n.value), src, dst
+
+
+def from_edges_undirected(n: int, edges, dtype: int = U32) -> Csr:
+    """CsrMatrix::from_edges_undirected (src/graph_csr.rs:138-147)."""
+    e = np.asarray(edges, dtype=np.int64).reshape(-1, 2)
+    off = e[:, 0] != e[:, 1]
+    r = np.empty(len(e) + int(off.sum()), np.int64)
+    c = np.empty_like(r)
+    # triplet order (r,c) then (c,r) per edge, as the reference pushes them
+    idx = np.arange(len(e)) + np.concatenate([[0], np.cumsum(off)[:-1]]) if len(e) else np.zeros(0, np.int64)
+    r[idx], c[idx] = e[:, 0], e[:, 1]
+    r[idx[off] + 1], c[idx[off] + 1] = e[off, 1], e[off, 0]
+    return from_coo(n, r, c, np.ones(len(r)), dtype)
 
 
 def torus_thinned(side: int, epn: float, rng: Rng) -> Csr:

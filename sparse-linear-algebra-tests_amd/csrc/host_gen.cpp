@@ -9,6 +9,7 @@
 //   slat_host_thin      CsrMatrix::thin       src/graph_csr.rs:225-247
 //   slat_host_rmat      seeded R-MAT for the f64 power-law config (not in the reference)
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -306,3 +307,68 @@ slat_status slat_host_rmat(uint32_t scale, uint64_t n_edges, double a, double b,
 }
 
 }  // extern "C"
+
+// load_edges (src/graph_csr.rs:1209-1224): the file read whole, lines trimmed, empty lines skipped,
+// the first two whitespace-separated tokens parsed as u32 (an optional '+', like str::parse);
+// n = max id + 1. A missing or malformed token -> SLAT_EINVAL (the reference panics).
+extern "C" slat_status slat_load_edges(const char *path, uint64_t *n, uint64_t *n_edges, uint32_t **src,
+                                       uint32_t **dst) {
+    if (!path || !n || !n_edges || !src || !dst) return SLAT_EINVAL;
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return SLAT_EINVAL;
+    std::vector<char> buf;
+    char chunk[1 << 16];
+    size_t got;
+    while ((got = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + got);
+    std::fclose(f);
+    buf.push_back('\n');
+    auto space = [](char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\f' || c == '\v'; };
+    std::vector<uint32_t> s, d;
+    uint32_t max_id = 0;
+    size_t i = 0;
+    const size_t end = buf.size();
+    while (i < end) {
+        uint64_t v[2];
+        int tokens = 0;
+        while (true) {
+            while (i < end && space(buf[i])) ++i;
+            if (i >= end || buf[i] == '\n' || tokens == 2) break;
+            if (buf[i] == '+') ++i;
+            if (i >= end || buf[i] < '0' || buf[i] > '9') return SLAT_EINVAL;
+            uint64_t x = 0;
+            while (i < end && buf[i] >= '0' && buf[i] <= '9') {
+                x = x * 10 + (uint64_t)(buf[i++] - '0');
+                if (x > 0xFFFFFFFFull) return SLAT_EINVAL;
+            }
+            if (i < end && buf[i] != '\n' && !space(buf[i])) return SLAT_EINVAL;
+            v[tokens++] = x;
+        }
+        while (i < end && buf[i] != '\n') ++i;  // further tokens are not read
+        ++i;
+        if (tokens == 0) continue;
+        if (tokens == 1) return SLAT_EINVAL;
+        s.push_back((uint32_t)v[0]);
+        d.push_back((uint32_t)v[1]);
+        max_id = std::max(max_id, std::max((uint32_t)v[0], (uint32_t)v[1]));
+    }
+    if (max_id == 0xFFFFFFFFu) return SLAT_EINVAL;  // max_id + 1 overflows NodeId
+    *src = (uint32_t *)std::malloc(std::max<size_t>(s.size(), 1) * 4);
+    *dst = (uint32_t *)std::malloc(std::max<size_t>(d.size(), 1) * 4);
+    if (!*src || !*dst) {
+        std::free(*src);
+        std::free(*dst);
+        return SLAT_EOOM;
+    }
+    if (!s.empty()) {
+        std::memcpy(*src, s.data(), s.size() * 4);
+        std::memcpy(*dst, d.data(), d.size() * 4);
+    }
+    *n = (uint64_t)max_id + 1;
+    *n_edges = s.size();
+    return SLAT_OK;
+}
+
+extern "C" void slat_edges_free(uint32_t *src, uint32_t *dst) {
+    std::free(src);
+    std::free(dst);
+}

@@ -4,7 +4,7 @@
 //   1. C.row_ptr and C.col/val in one device block of the context's cache (slat_dev_alloc). By
 //      default C is sized by the exact upper bound nnz(A)·max_row_nnz(B) (clamped to rows·cols),
 //      so no host round trip is needed between the symbolic and numeric passes; the capacity is
-//      recorded in slat_csr.capacity. SLAT_FLAG_EXACT_ALLOC (or a bound above the memory budget)
+//      recorded in slat_csr.capacity. SLAT_FLAG_EXACT_ALLOC (or a bound above 4 GiB / the budget)
 //      takes the reference's exact-size path instead: sync after the scan, allocate nnz(C).
 //   2. k_symbolic -> k_scan_rows (single-pass look-back scan) -> k_numeric, all stream-ordered.
 //   3. One D2H of the 64 status shards (nnz, max row nnz, dropped-zero rows) + stream sync.
@@ -22,6 +22,9 @@
 #include "spgemm_kernels.hpp"
 
 using namespace slat;
+
+// max(B) for the CSR walk too (SLAT_NO_NARROW_CSR=1: the u64 slots of before, for A/B runs)
+static const bool kNarrowCsr = std::getenv("SLAT_NO_NARROW_CSR") == nullptr;
 
 extern "C" {
 
@@ -646,6 +649,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             a.b_vmax = ctx->d_vmax;
             a.epoch = ++ctx->epoch;
         }
+    } else if (dt == SLAT_U32 && kNarrowCsr) {
+        // B walked in CSR form: k_bvmax gives the numeric pass the same max(B) (narrow slots, and
+        // hub rows accumulate in C instead of one re-traversal per rank chunk)
+        a.b_vmax = ctx->d_vmax;
+        a.epoch = ++ctx->epoch;
     }
     a.counts = (uint64_t *)ws;
     a.shards = (unsigned long long *)(ws + o_sh);
@@ -662,7 +670,13 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const unsigned __int128 dense = (unsigned __int128)n * ncols;
     if (bound128 > dense) bound128 = dense;
     // free device memory: refreshed every 32 calls above (the query costs host time on every call)
-    const unsigned __int128 budget = (unsigned __int128)ctx->free_b / 4;
+    // and at most kBoundBytes: a loose bound (power-law B: nnz(A) x a hub row) would make every call
+    // allocate and release tens of GB, which costs far more than the exact path's one sync
+    static const uint64_t kBoundBytes = [] {
+        const char *e = std::getenv("SLAT_BOUND_MAX_BYTES");
+        return e ? std::strtoull(e, nullptr, 10) : (4ull << 30);
+    }();
+    const unsigned __int128 budget = std::min<unsigned __int128>(ctx->free_b / 4, kBoundBytes);
     const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
     if (!exact) {
         C->capacity = (uint64_t)std::max<unsigned __int128>(bound128, 1);
@@ -694,6 +708,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         else
             be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, ctx->d_vmax, a.epoch);
         SLAT_HIP(ctx, be);
+    } else if (a.b_vmax && B->nnz) {
+        const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
+        hipLaunchKernelGGL(k_bvmax, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz, ctx->d_vmax,
+                           a.epoch);
+        SLAT_HIP(ctx, hipGetLastError());
     }
     if (ablate & 7u) {
         // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded

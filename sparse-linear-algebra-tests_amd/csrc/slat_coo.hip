@@ -10,7 +10,9 @@
 // (u64 draws only, so never split across refills), hence every draw is computed independently.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
+#include <vector>
 #include <hipcub/hipcub.hpp>
 
 #include "slat.h"
@@ -60,7 +62,7 @@ __global__ void k_coo_heads(const uint64_t *keys, uint64_t nt, uint64_t n, uint6
 // every head sums its run in sorted (= input) order; keep = the sum is not zero
 __global__ void k_coo_runs(const uint64_t *keys, const uint32_t *idx, const void *vals, int dt, uint64_t nt,
                            const uint64_t *head, const uint64_t *upos, uint64_t *ukey, uint64_t *uval,
-                           uint64_t *keep) {
+                           uint64_t *keep, int keep_zeros) {
     for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < nt; i += (uint64_t)gridDim.x * kB) {
         if (!head[i]) continue;
         const uint64_t k = keys[i];
@@ -70,7 +72,7 @@ __global__ void k_coo_runs(const uint64_t *keys, const uint32_t *idx, const void
         if (u >= nt) continue;  // never write outside the run arrays (a scan gone wrong stays a wrong result)
         ukey[u] = k;
         uval[u] = v;
-        keep[u] = zero_bits(v, dt) ? 0u : 1u;
+        keep[u] = keep_zeros || !zero_bits(v, dt) ? 1u : 0u;
     }
 }
 
@@ -245,7 +247,7 @@ slat_status scan_total(slat_ctx *ctx, const uint64_t *cnt, uint64_t n, uint64_t 
 
 // from_coo core over device triplets (rows, cols, value bits `vals` of dtype dt: u32 or u64 words)
 slat_status from_coo_dev(slat_ctx *ctx, uint64_t n, uint64_t nt, const uint32_t *rows, const uint32_t *cols,
-                         const void *vals, int32_t dt, slat_csr *out, int skip = 0) {
+                         const void *vals, int32_t dt, slat_csr *out, int skip = 0, int keep_zeros = 0) {
     hipStream_t s = ctx->stream;
     std::memset(out, 0, sizeof *out);
     out->n_rows = out->n_cols = n;
@@ -293,7 +295,7 @@ slat_status from_coo_dev(slat_ctx *ctx, uint64_t n, uint64_t nt, const uint32_t 
     slat_status st;
     if ((st = scan_total(ctx, head, nt, upos, &nu))) return st;
     if (ctx->h_out[3]) return fail(ctx, SLAT_EINVAL, "from_coo: row or column id >= n");  // the reference panics
-    hipLaunchKernelGGL(k_coo_runs, g, b, 0, s, k2, i2, vals, dt, nt, head, upos, ukey, uval, keep);
+    hipLaunchKernelGGL(k_coo_runs, g, b, 0, s, k2, i2, vals, dt, nt, head, upos, ukey, uval, keep, keep_zeros);
     SLAT_HIP(ctx, hipGetLastError());
     if ((st = scan_total(ctx, keep, nu, fpos, &nnz))) return st;
     SLAT_HIP(ctx, alloc_joint(ctx, out, n, nnz, vs, s));
@@ -407,4 +409,257 @@ extern "C" slat_status slat_csr_thin(slat_ctx *ctx, const slat_csr_view *m, slat
         vals = tnar;
     }
     return from_coo_dev(ctx, n, ntrip, trow, tcol, vals, m->dtype, out);
+}
+
+// ------------------------------------------------------------------------------------------------
+// The real-graph path: edge lists to CSR, the RCM order, the symmetric
+// permutation and the bandwidth statistics, on the device except the order itself (a sequential
+// BFS, computed on the host like the reference's).
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ void flag_bad(unsigned long long *bad) {
+    __hip_atomic_store(bad, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// inv[perm[k]] = k; ids >= n flagged
+__global__ void k_perm_inverse(const uint32_t *perm, uint64_t n, uint32_t *inv, unsigned long long *bad) {
+    for (uint64_t k = (uint64_t)blockIdx.x * kB + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kB) {
+        const uint32_t p = perm[k];
+        if (p >= n) flag_bad(bad); else inv[p] = (uint32_t)k;
+    }
+}
+// a repeated id leaves inv pointing at only one of its positions
+__global__ void k_perm_check(const uint32_t *perm, uint64_t n, const uint32_t *inv, unsigned long long *bad) {
+    for (uint64_t k = (uint64_t)blockIdx.x * kB + threadIdx.x; k < n; k += (uint64_t)gridDim.x * kB) {
+        const uint32_t p = perm[k];
+        if (p < n && inv[p] != (uint32_t)k) flag_bad(bad);
+    }
+}
+// entry i of row r -> (inv[r], inv[col], value bits)
+__global__ void k_perm_trip(const uint64_t *rp, const uint32_t *col, const void *val, int dt, uint64_t n,
+                            uint64_t nnz, const uint32_t *inv, uint32_t *trow, uint32_t *tcol, uint64_t *tval) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < nnz; i += (uint64_t)gridDim.x * kB) {
+        trow[i] = inv[row_of(rp, n, i)];
+        tcol[i] = inv[col[i]];
+        tval[i] = load_bits(val, i, dt);
+    }
+}
+// from_edges / from_edges_undirected (src/graph_csr.rs:132-147): (r, c, 1) then, undirected and
+// r != c, (c, r, 1) in the second half (row 0xFFFFFFFF = no triplet); ids >= n flagged
+__global__ void k_edges_trip(const uint32_t *src, const uint32_t *dst, uint64_t m, uint64_t n, int undirected,
+                             uint32_t *trow, uint32_t *tcol, uint32_t *tval, unsigned long long *bad) {
+    for (uint64_t e = (uint64_t)blockIdx.x * kB + threadIdx.x; e < m; e += (uint64_t)gridDim.x * kB) {
+        const uint32_t r = src[e], c = dst[e];
+        if (r >= n || c >= n) flag_bad(bad);
+        trow[e] = r;
+        tcol[e] = c;
+        tval[e] = 1u;
+        if (undirected) {
+            trow[m + e] = r != c ? c : 0xFFFFFFFFu;
+            tcol[m + e] = r;
+            tval[m + e] = 1u;
+        }
+    }
+}
+// bandwidth_stats (src/graph_csr.rs:802-818): max and sum of |r - c|
+__global__ void k_bandwidth(const uint64_t *rp, const uint32_t *col, uint64_t n, uint64_t nnz,
+                            unsigned long long *out) {
+    unsigned long long mx = 0, sum = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < nnz; i += (uint64_t)gridDim.x * kB) {
+        const uint64_t r = row_of(rp, n, i), c = col[i], d = r > c ? r - c : c - r;
+        mx = mx > d ? mx : d;
+        sum += d;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long om = __shfl_xor(mx, o), os = __shfl_xor(sum, o);
+        mx = mx > om ? mx : om;
+        sum += os;
+    }
+    if ((threadIdx.x & 63) == 0 && (mx || sum)) {
+        atomicMax(&out[0], mx);
+        atomicAdd(&out[1], sum);
+    }
+}
+
+// device or host u32 array -> device pointer (staged into `buf` when host)
+slat_status device_u32(slat_ctx *ctx, const uint32_t *p, uint64_t count, int32_t residency, Buf &buf,
+                       const uint32_t **out) {
+    if (residency == SLAT_DEVICE) {
+        *out = p;
+        return SLAT_OK;
+    }
+    if (buf.alloc(count * 4 + 64) != hipSuccess) return fail(ctx, SLAT_EOOM, "staging");
+    if (count) SLAT_HIP(ctx, hipMemcpyAsync(buf.p, p, count * 4, hipMemcpyHostToDevice, ctx->stream));
+    *out = (const uint32_t *)buf.p;
+    return SLAT_OK;
+}
+
+}  // namespace
+
+extern "C" slat_status slat_csr_permute(slat_ctx *ctx, const slat_csr_view *m, const uint32_t *perm,
+                                        int32_t perm_residency, slat_csr *out) {
+    if (!ctx || !out || (!perm && m && m->n_rows)) return SLAT_EINVAL;
+    slat_status st = slat_check_view(ctx, m, "m");
+    if (st) return st;
+    if (m->residency != SLAT_DEVICE) return fail(ctx, SLAT_EINVAL, "permute takes a device-resident matrix");
+    if (m->n_rows != m->n_cols) return fail(ctx, SLAT_EDIM, "matrix is not square");
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const uint64_t n = m->n_rows, nnz = m->nnz;
+    Buf stage{ctx}, scratch{ctx};
+    const uint32_t *dperm = nullptr;
+    if ((st = device_u32(ctx, perm, n, perm_residency, stage, &dperm))) return st;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_tr = up(std::max<uint64_t>(n, 1) * 4), o_tc = o_tr + up(nnz * 4), o_tv = o_tc + up(nnz * 4),
+                 o_tn = o_tv + up(nnz * 8), total_b = o_tn + up(nnz * 4) + 256;
+    if (scratch.alloc(total_b) != hipSuccess) return fail(ctx, SLAT_EOOM, "permute scratch");
+    uint8_t *w = (uint8_t *)scratch.p;
+    uint32_t *inv = (uint32_t *)w, *trow = (uint32_t *)(w + o_tr), *tcol = (uint32_t *)(w + o_tc),
+             *tnar = (uint32_t *)(w + o_tn);
+    uint64_t *tval = (uint64_t *)(w + o_tv);
+    const dim3 b(kB);
+    ctx->h_out[3] = 0;
+    if (n) {
+        hipLaunchKernelGGL(k_perm_inverse, grid_for(ctx, n), b, 0, s, dperm, n, inv, ctx->h_out_dev + 3);
+        hipLaunchKernelGGL(k_perm_check, grid_for(ctx, n), b, 0, s, dperm, n, inv, ctx->h_out_dev + 3);
+        SLAT_HIP(ctx, hipGetLastError());
+        SLAT_HIP(ctx, hipStreamSynchronize(s));
+        if (ctx->h_out[3]) return fail(ctx, SLAT_EINVAL, "permute: perm is not a permutation of 0..n");
+    }
+    const void *vals = tval;
+    if (nnz) {
+        hipLaunchKernelGGL(k_perm_trip, grid_for(ctx, nnz), b, 0, s, m->row_ptr, m->col_idx, m->values, m->dtype,
+                           n, nnz, inv, trow, tcol, tval);
+        SLAT_HIP(ctx, hipGetLastError());
+        if (m->dtype == SLAT_U32) {
+            hipLaunchKernelGGL(k_narrow_u32, grid_for(ctx, nnz), b, 0, s, tval, nnz, tnar);
+            SLAT_HIP(ctx, hipGetLastError());
+            vals = tnar;
+        }
+    }
+    // a permutation maps distinct entries to distinct entries: from_coo only sorts (zeros kept)
+    return from_coo_dev(ctx, n, nnz, trow, tcol, vals, m->dtype, out, 0, 1);
+}
+
+extern "C" slat_status slat_csr_from_edges(slat_ctx *ctx, uint64_t n, uint64_t n_edges, const uint32_t *src,
+                                           const uint32_t *dst, int32_t undirected, int32_t residency,
+                                           slat_csr *out) {
+    if (!ctx || !out) return SLAT_EINVAL;
+    if (n_edges && (!src || !dst)) return fail(ctx, SLAT_EINVAL, "from_edges: null arrays");
+    if (n > 0xFFFFFFFFull) return fail(ctx, SLAT_EINVAL, "n exceeds u32 ids");
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    Buf s_src{ctx}, s_dst{ctx}, scratch{ctx};
+    const uint32_t *ds = nullptr, *dd = nullptr;
+    slat_status st;
+    if ((st = device_u32(ctx, src, n_edges, residency, s_src, &ds))) return st;
+    if ((st = device_u32(ctx, dst, n_edges, residency, s_dst, &dd))) return st;
+    const uint64_t nt = undirected ? 2 * n_edges : n_edges;
+    if (scratch.alloc(nt * 12 + 256) != hipSuccess) return fail(ctx, SLAT_EOOM, "from_edges triplets");
+    uint32_t *trow = (uint32_t *)scratch.p, *tcol = trow + nt, *tval = tcol + nt;
+    ctx->h_out[3] = 0;
+    if (n_edges) {
+        hipLaunchKernelGGL(k_edges_trip, grid_for(ctx, n_edges), dim3(kB), 0, s, ds, dd, n_edges, n, undirected,
+                           trow, tcol, tval, ctx->h_out_dev + 3);
+        SLAT_HIP(ctx, hipGetLastError());
+        SLAT_HIP(ctx, hipStreamSynchronize(s));
+        if (ctx->h_out[3]) return fail(ctx, SLAT_EINVAL, "from_edges: node id >= n");  // the reference panics
+    }
+    return from_coo_dev(ctx, n, nt, trow, tcol, tval, SLAT_U32, out, 1);
+}
+
+extern "C" slat_status slat_bandwidth_stats(slat_ctx *ctx, const slat_csr_view *m, uint64_t *max_bw,
+                                            double *avg_bw) {
+    if (!ctx || !max_bw || !avg_bw) return SLAT_EINVAL;
+    slat_status st = slat_check_view(ctx, m, "m");
+    if (st) return st;
+    if (m->residency != SLAT_DEVICE) return fail(ctx, SLAT_EINVAL, "bandwidth_stats takes a device-resident matrix");
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    Buf acc{ctx};
+    if (acc.alloc(16) != hipSuccess) return fail(ctx, SLAT_EOOM, "bandwidth accumulators");
+    unsigned long long h[2] = {0, 0};
+    SLAT_HIP(ctx, hipMemsetAsync(acc.p, 0, 16, s));
+    if (m->nnz) {
+        hipLaunchKernelGGL(k_bandwidth, grid_for(ctx, m->nnz), dim3(kB), 0, s, m->row_ptr, m->col_idx, m->n_rows,
+                           m->nnz, (unsigned long long *)acc.p);
+        SLAT_HIP(ctx, hipGetLastError());
+    }
+    SLAT_HIP(ctx, hipMemcpyAsync(h, acc.p, 16, hipMemcpyDeviceToHost, s));
+    SLAT_HIP(ctx, hipStreamSynchronize(s));
+    *max_bw = h[0];
+    *avg_bw = (double)h[1] / (double)std::max<uint64_t>(m->nnz, 1);
+    return SLAT_OK;
+}
+
+// CsrMatrix::rcm's order (src/graph_csr.rs:663-722), perm[new] = old: per unvisited seed, a plain
+// BFS whose last node starts a BFS that takes unvisited neighbours by ascending degree (ties in
+// column order, i.e. a stable sort: the reference's sort_unstable leaves ties unspecified); the
+// visit order reversed. The BFS is sequential, so it runs on the host over a host copy.
+extern "C" slat_status slat_rcm_order(slat_ctx *ctx, const slat_csr_view *m, uint32_t *perm) {
+    if (!ctx || !perm) return SLAT_EINVAL;
+    slat_status st = slat_check_view(ctx, m, "m");
+    if (st) return st;
+    if (m->n_rows != m->n_cols) return fail(ctx, SLAT_EDIM, "matrix is not square");
+    const uint64_t n = m->n_rows;
+    std::vector<uint64_t> rp_h;
+    std::vector<uint32_t> col_h;
+    const uint64_t *rp = m->row_ptr;
+    const uint32_t *col = m->col_idx;
+    if (m->residency == SLAT_DEVICE) {
+        SLAT_HIP(ctx, hipSetDevice(ctx->device));
+        rp_h.resize(n + 1);
+        col_h.resize(std::max<uint64_t>(m->nnz, 1));
+        SLAT_HIP(ctx, hipMemcpyAsync(rp_h.data(), m->row_ptr, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (m->nnz)
+            SLAT_HIP(ctx, hipMemcpyAsync(col_h.data(), m->col_idx, m->nnz * 4, hipMemcpyDeviceToHost, ctx->stream));
+        SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        rp = rp_h.data();
+        col = col_h.data();
+    }
+    if (n == 0) return SLAT_OK;
+    auto deg = [&](uint64_t v) { return rp[v + 1] - rp[v]; };
+    std::vector<uint8_t> visited(n, 0);
+    std::vector<uint64_t> mark(n, 0), queue, order, nbrs;
+    queue.reserve(n);
+    order.reserve(n);
+    for (uint64_t seed = 0; seed < n; ++seed) {
+        if (visited[seed]) continue;
+        // pseudo-peripheral start: the last node of a BFS from the seed (its own visited marks)
+        queue.clear();
+        queue.push_back(seed);
+        mark[seed] = seed + 1;
+        uint64_t last = seed;
+        for (size_t h = 0; h < queue.size(); ++h) {
+            const uint64_t u = queue[h];
+            last = u;
+            for (uint64_t i = rp[u]; i < rp[u + 1]; ++i)
+                if (mark[col[i]] != seed + 1) {
+                    mark[col[i]] = seed + 1;
+                    queue.push_back(col[i]);
+                }
+        }
+        queue.clear();
+        queue.push_back(last);
+        visited[last] = 1;
+        for (size_t h = 0; h < queue.size(); ++h) {
+            const uint64_t u = queue[h];
+            order.push_back(u);
+            if (order.size() > n) return fail(ctx, SLAT_EINVAL, "rcm: order is not a permutation");
+            nbrs.clear();
+            for (uint64_t i = rp[u]; i < rp[u + 1]; ++i)
+                if (!visited[col[i]]) nbrs.push_back(col[i]);
+            std::stable_sort(nbrs.begin(), nbrs.end(), [&](uint64_t x, uint64_t y) { return deg(x) < deg(y); });
+            for (uint64_t v : nbrs)
+                if (!visited[v]) {
+                    visited[v] = 1;
+                    queue.push_back(v);
+                }
+        }
+    }
+    // a directed graph can restart a finished component: the reference's permute then panics
+    if (order.size() != n) return fail(ctx, SLAT_EINVAL, "rcm: order is not a permutation");
+    for (uint64_t i = 0; i < n; ++i) perm[i] = (uint32_t)order[n - 1 - i];
+    return SLAT_OK;
 }

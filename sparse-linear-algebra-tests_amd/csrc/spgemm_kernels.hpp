@@ -380,6 +380,33 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
     }
 }
 
+// the same B-value summary when B is walked in CSR form (no ELL copy): max and ~min of the u32
+// values, epoch-tagged, one atomic pair per block
+static __global__ __launch_bounds__(kBlock) void k_bvmax(const uint32_t *val, uint64_t nnz,
+                                                          unsigned long long *vmax, uint32_t epoch) {
+    uint32_t mx = 0, mn = 0xFFFFFFFFu;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nnz; i += (uint64_t)gridDim.x * kBlock) {
+        mx = max(mx, val[i]);
+        mn = min(mn, val[i]);
+    }
+    __shared__ uint32_t bm[kBlock / kWave], bn[kBlock / kWave];
+    mx = wave_max_u32(mx);
+    mn = wave_min_u32(mn);
+    if (lane_id() == 0) {
+        bm[threadIdx.x / kWave] = mx;
+        bn[threadIdx.x / kWave] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) {
+            mx = max(mx, bm[w]);
+            mn = min(mn, bn[w]);
+        }
+        atomicMax(&vmax[kVMaxWord], ((unsigned long long)epoch << 32) | mx);
+        atomicMax(&vmax[kVMinInvWord], ((unsigned long long)epoch << 32) | ~mn);
+    }
+}
+
 template <typename S>
 struct Quad {
     S v[4];
@@ -1274,7 +1301,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     uint32_t bvmax = 0xFFFFFFFFu;  // max B value of this call (u32 semiring with the ELL copy)
     bool buni = false;             // every B value equals bvmax (a pattern B)
     if constexpr (Sem::kNarrowable)
-        if (ELL && p.b_vmax) {
+        if (p.b_vmax) {
             const unsigned long long v = ((volatile unsigned long long *)p.b_vmax)[kVMaxWord];
             const unsigned long long vi = ((volatile unsigned long long *)p.b_vmax)[kVMinInvWord];
             if ((uint32_t)(v >> 32) == p.epoch) {
@@ -1453,8 +1480,16 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 // max(A row) * max(B) * len(A row) < 2^32 (each output sums <= len products)
                 bool narrow = false;
                 if constexpr (Sem::kNarrowable) {
-                    if (ELL && bvmax != 0xFFFFFFFFu) {
-                        const uint64_t x = (uint64_t)wave_max_u32(rw.amax) * bvmax;
+                    // (rw.amax covers the row once its segments went through load_seg: always
+                    // with ELL and for one-segment rows; a longer row in the CSR walk reads its A
+                    // values once more here)
+                    if (bvmax != 0xFFFFFFFFu) {
+                        uint32_t am = rw.amax;
+                        if (!ELL && !rw.single) {
+                            const uint32_t *av = (const uint32_t *)p.a_val;
+                            for (I j = a0 + (I)lane; j < a1; j += (I)kWave) am = max(am, av[j]);
+                        }
+                        const uint64_t x = (uint64_t)wave_max_u32(am) * bvmax;
                         narrow = x == 0 || len <= 0xFFFFFFFFull / x;
                     }
                 }
@@ -1522,7 +1557,12 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 auto run_chunks = [&](auto narrow_tag, auto uni_tag) {
                     constexpr bool NW = decltype(narrow_tag)::value;
                     const uint32_t cap = NW ? cap_n : cap_w;
-                    if constexpr (GlobalOverflow<Sem>::value) {
+                    // u32 rows under the narrow bound cannot overflow a u32 sum, so their atomics
+                    // in C are exact too: no re-traversal per rank chunk for hub rows (B walked in
+                    // CSR form; the ELL instances keep their registers: +3 us on the 30^3 bench)
+                    constexpr bool kGO =
+                        GlobalOverflow<Sem>::value || (std::is_same<Sem, SemU32>::value && NW && !ELL);
+                    if constexpr (kGO) {
                         if (wcnt > cap) {
                             // one pass into the C slice: zero it, then global atomics at out + rank
                             uint32_t *oc = p.c_col + out_pos;
@@ -1532,7 +1572,10 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                             __builtin_amdgcn_s_waitcnt(0);  // the zeros reach L2 before the atomics
                             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                             GlobalAcc<Sem> ga{W, p.ww, Z ? 0u : wlo, lim, oc, ov};
-                            rw.template each_group<true>(ga);
+                            if constexpr (NW)
+                                rw.template each_group<true, SemU32Narrow, decltype(uni_tag)::value>(ga, bv0);
+                            else
+                                rw.template each_group<true>(ga);
                             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
                             // zero sums (cancellation) are counted by the compaction test below
                             for (uint32_t t = lane; t < lim; t += kWave) {
@@ -1554,6 +1597,11 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                     if (narrow && buni)
                         run_chunks(std::true_type{}, std::true_type{});
                     else if (narrow)
+                        run_chunks(std::true_type{}, std::false_type{});
+                    else
+                        run_chunks(std::false_type{}, std::false_type{});
+                } else if constexpr (Sem::kNarrowable) {  // B in CSR form: values always loaded
+                    if (narrow)
                         run_chunks(std::true_type{}, std::false_type{});
                     else
                         run_chunks(std::false_type{}, std::false_type{});

@@ -24,6 +24,8 @@ EXPORTS = [
     "slat_host_from_coo", "slat_host_lattice", "slat_host_thin", "slat_host_rmat", "slat_host_csr_free",
     "slat_csr_add", "slat_csr_identity", "slat_csr_pattern_equal", "slat_reachability_sum",
     "slat_power_until_stable", "slat_connected_components", "slat_csr_from_coo", "slat_csr_lattice", "slat_csr_thin",
+    "slat_load_edges", "slat_edges_free", "slat_csr_from_edges", "slat_rcm_order", "slat_csr_permute",
+    "slat_bandwidth_stats",
 ]
 
 
@@ -119,6 +121,12 @@ def lib():
         "slat_csr_from_coo": ([vp, u64, u64, vp, vp, vp, i32, i32, P(CsrOwned)], C.c_int),
         "slat_csr_lattice": ([vp, P(u64), C.c_int, C.c_int, P(CsrOwned)], C.c_int),
         "slat_csr_thin": ([vp, P(CsrView), P(RngState), C.c_double, P(CsrOwned)], C.c_int),
+        "slat_load_edges": ([C.c_char_p, P(u64), P(u64), P(vp), P(vp)], C.c_int),
+        "slat_edges_free": ([vp, vp], None),
+        "slat_csr_from_edges": ([vp, u64, u64, vp, vp, i32, i32, P(CsrOwned)], C.c_int),
+        "slat_rcm_order": ([vp, P(CsrView), vp], C.c_int),
+        "slat_csr_permute": ([vp, P(CsrView), vp, i32, P(CsrOwned)], C.c_int),
+        "slat_bandwidth_stats": ([vp, P(CsrView), P(u64), P(C.c_double)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

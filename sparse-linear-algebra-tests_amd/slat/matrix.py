@@ -168,6 +168,19 @@ def host_rmat(scale: int, n_edges: int, a=0.57, b=0.19, c=0.19, seed: bytes = by
     return HostCsr._take(h)
 
 
+def load_edges(path: str):
+    """load_edges (src/graph_csr.rs:1209-1224) -> (n, src u32[], dst u32[]); n = max id + 1."""
+    n, m, s, d = C.c_uint64(), C.c_uint64(), C.c_void_p(), C.c_void_p()
+    L.check(L.lib().slat_load_edges(str(path).encode(), C.byref(n), C.byref(m), C.byref(s), C.byref(d)))
+    k = int(m.value)
+    try:
+        src = np.ctypeslib.as_array(C.cast(s, C.POINTER(C.c_uint32)), (max(k, 1),))[:k].copy()
+        dst = np.ctypeslib.as_array(C.cast(d, C.POINTER(C.c_uint32)), (max(k, 1),))[:k].copy()
+    finally:
+        L.lib().slat_edges_free(s, d)
+    return int(n.value), src, dst
+
+
 def torus_thinned(side: int, epn: float, rng: StdRng) -> HostCsr:
     """side^3 Moore torus thinned to `epn` edges per node (src/graph_magnus.rs:713-719)."""
     full = host_lattice([side, side, side], True)
@@ -283,6 +296,64 @@ class DeviceCsr:
         L.check(L.lib().slat_csr_from_coo(ctx.ptr, n, len(r), r.ctypes.data, c.ctypes.data, v.ctypes.data, cls.DTYPE,
                                           L.HOST, C.byref(out)), ctx.ptr)
         return cls(out, ctx)
+
+    @classmethod
+    def from_edges_device(cls, n: int, src, dst, undirected: bool = False, ctx: Context | None = None):
+        """CsrMatrix::from_edges / from_edges_undirected (src/graph_csr.rs:132-147) on the device."""
+        ctx = ctx or default_context()
+        s = np.ascontiguousarray(src, np.uint32)
+        d = np.ascontiguousarray(dst, np.uint32)
+        if len(s) != len(d):
+            raise ValueError("src and dst differ in length")
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_from_edges(ctx.ptr, n, len(s), s.ctypes.data, d.ctypes.data, int(undirected),
+                                            L.HOST, C.byref(out)), ctx.ptr)
+        m = CsrMatrix(out, ctx)
+        return m if cls.DTYPE == L.U32 else cls.from_host(m.host().astype(cls.DTYPE), ctx)
+
+    # -- reordering (src/graph_csr.rs:663-818) -------------------------------------------------------
+    perm = None  # perm[new] = old after permute / rcm, like the reference's `perm` field
+
+    def rcm_order(self) -> np.ndarray:
+        """The order CsrMatrix::rcm permutes by (perm[new] = old); degree ties in column order."""
+        p = np.zeros(max(self.n, 1), np.uint32)
+        v = self.view()
+        L.check(L.lib().slat_rcm_order(self._ctx.ptr, C.byref(v), p.ctypes.data), self._ctx.ptr)
+        return p[:self.n]
+
+    def permute(self, perm):
+        """CsrMatrix::permute (src/graph_csr.rs:726-783), in place; stores `perm`."""
+        p = np.ascontiguousarray(perm, np.uint32)
+        if len(p) != self.n:
+            raise ValueError("perm length != n")  # assert_eq!(perm.len(), nu)
+        v = self.view()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_csr_permute(self._ctx.ptr, C.byref(v), p.ctypes.data, L.HOST, C.byref(out)),
+                self._ctx.ptr)
+        L.lib().slat_csr_free(self._ctx.ptr, C.byref(self._m))
+        self._m = out
+        self._host = None
+        self.perm = p.copy()
+
+    def rcm(self):
+        """CsrMatrix::rcm (src/graph_csr.rs:663-722), in place; stores the permutation."""
+        self.permute(self.rcm_order())
+
+    def unpermute(self):
+        """CsrMatrix::unpermute (src/graph_csr.rs:786-799): permute by the inverse, drop `perm`."""
+        if self.perm is None:
+            return
+        inv = np.empty_like(self.perm)
+        inv[self.perm] = np.arange(len(self.perm), dtype=np.uint32)
+        self.permute(inv)
+        self.perm = None
+
+    def bandwidth_stats(self):
+        """CsrMatrix::bandwidth_stats (src/graph_csr.rs:802-818) -> (max |r-c|, mean |r-c|)."""
+        mx, avg = C.c_uint64(), C.c_double()
+        v = self.view()
+        L.check(L.lib().slat_bandwidth_stats(self._ctx.ptr, C.byref(v), C.byref(mx), C.byref(avg)), self._ctx.ptr)
+        return int(mx.value), float(avg.value)
 
     # -- accessors ---------------------------------------------------------------------------------
     @property

@@ -283,3 +283,21 @@ def test_timing_stats(ctx):
     st = ctx.stats()
     assert st["nnz"] == 251590 and st["flops"] == 317168
     assert st["numeric_ms"] > 0 and st["symbolic_ms"] > 0
+
+
+@pytest.mark.parametrize("vmax", [3, 1 << 14, 1 << 20])
+@pytest.mark.parametrize("wide", [False, True])
+def test_u32_csr_walk_narrow_and_hub_rows(ctx, vmax, wide):
+    # B rows longer than the ELL limit (CSR walk) with k_bvmax's max(B): small values take narrow
+    # slots and hub rows (more outputs than slots) accumulate in C; 2^20 values saturate products
+    # and sums (u64 slots, rank chunks). wide: more columns than one LDS window.
+    n = 70_000 if wide else 6000
+    g = np.random.default_rng(vmax + wide)
+    rows = np.concatenate([g.integers(0, n, 6 * n), np.zeros(3000, np.int64), np.full(800, 1)])
+    cols = np.concatenate([g.integers(0, n, 6 * n), g.integers(0, n, 3000), g.integers(0, n, 800)])
+    b_rows = np.concatenate([rows, np.repeat(np.arange(40), 120)])
+    b_cols = np.concatenate([cols, g.integers(0, n, 40 * 120)])
+    a = O.from_coo(n, rows, cols, g.integers(1, vmax + 1, len(rows)), O.U32)
+    b = O.from_coo(n, b_rows, b_cols, g.integers(1, vmax + 1, len(b_rows)), O.U32)
+    got = to_dev(a, slat.U32).matmul(to_dev(b, slat.U32))
+    assert_same(got, O.matmul_seq(a, b), f"csr walk vmax={vmax} wide={wide}")

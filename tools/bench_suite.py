@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=2.0, help="seconds of timed CPU calls per cell")
     ap.add_argument("--cpu-max-nnz", type=float, default=3e7, help="skip the CPU leg above this nnz(A)")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
-    ap.add_argument("--only", default="GEN,C1,C2,C3,C4,C5")
+    ap.add_argument("--only", default="GEN,C1,C2,C3,C4,C5,RG")
     ap.add_argument("--rmat-scale", type=int, default=16)
     ap.add_argument("--rmat-deg", type=int, default=16)
     args = ap.parse_args()
@@ -171,6 +171,49 @@ def main():
                                  args, vs=8, flags=slat.FLAG_F64_ANY_ORDER, rtol=1e-12))
         out["cells"].append(cell(f"C5 rmat scale={scale} deg={deg} f64 A*A, reference fold order", dA, dA, oA, oA,
                                  args, vs=8))
+    if "RG" in only:
+        # the real-graph path (bench_real_graphs / analyze_graph_structure, src/graph_csr.rs:1427-1549)
+        # on synthetic stand-ins (the .edges files are absent): a power-law R-MAT graph made
+        # undirected, and a randomly numbered 50^3 torus. Edges -> device CSR, RCM, A^2 before/after.
+        g = np.random.default_rng(11)
+        h = slat.host_rmat(16, (1 << 16) * 8)
+        rows = np.repeat(np.arange(h.n, dtype=np.uint32), np.diff(h.row_ptr).astype(np.int64))
+        t = O.torus_thinned(50, 3.0, O.Rng())
+        tp = g.permutation(t.n).astype(np.uint32)
+        inv = np.empty_like(tp)
+        inv[tp] = np.arange(t.n, dtype=np.uint32)
+        trp, tcol, _ = t.arrays()
+        trows = np.repeat(np.arange(t.n, dtype=np.uint32), np.diff(trp).astype(np.int64))
+        for name, n, src, dst in [("rmat16 undirected", h.n, rows, h.col_idx),
+                                  ("torus50 renumbered", t.n, inv[trows], inv[tcol])]:
+            t0 = time.perf_counter()
+            dA = M.from_edges_device(n, src, dst, True, ctx)
+            t_build = time.perf_counter() - t0
+            oA = O.from_edges_undirected(n, np.stack([src, dst], 1)) if args.cpu else None
+            bw0 = dA.bandwidth_stats()
+            t0 = time.perf_counter()
+            p = dA.rcm_order()
+            t_order = time.perf_counter() - t0
+            dR = dA.clone()
+            t0 = time.perf_counter()
+            dR.permute(p)
+            t_perm = time.perf_counter() - t0
+            bw1 = dR.bandwidth_stats()
+            rec = {"graph": name, "n": n, "nnz": dA.nnz(), "from_edges_ms": t_build * 1e3, "rcm_order_ms": t_order * 1e3,
+                   "permute_ms": t_perm * 1e3, "bandwidth_before": bw0, "bandwidth_after": bw1}
+            if oA is not None:
+                rec["from_edges_exact"] = bool(same(dA, oA))
+                rec["rcm_order_equal"] = bool(np.array_equal(p, O.rcm_order(oA)))
+                oR = O.permute(oA, p)
+            else:
+                oR = _shape(dR.host())
+                oA = _shape(dA.host())
+            c0 = cell(f"RG {name} A^2", dA, dA, oA, oA, args)
+            c1 = cell(f"RG {name} A^2 after RCM", dR, dR, oR, oR, args)
+            rec.update({"a2_ms": c0["gpu_ms"], "a2_rcm_ms": c1["gpu_ms"]})
+            out["cells"] += [c0, c1]
+            print(json.dumps(rec), file=sys.stderr, flush=True)
+            out.setdefault("real_graph", []).append(rec)
 
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, "w") as f:
@@ -183,6 +226,12 @@ def main():
         print(f"| {r['cell']} | {r['nnz_c']} | {r['gpu_ms']:.3f} | {r['gnnz_s']:.2f} | {f('numeric_hbm_frac', '%.3f')} "
               f"| {f('pipeline_hbm_frac', '%.3f')} | {f('cpu_ms', '%.2f')} | {f('cpu_gnnz_s', '%.3f')} "
               f"| {f('speedup', '%.0f')} | {r.get('bit_exact', r.get('within_rtol_1e-12', '-'))} |")
+    for r in out.get("real_graph", []):
+        print(f"\n{r['graph']}: n {r['n']}, nnz {r['nnz']}; from_edges {r['from_edges_ms']:.1f} ms, rcm order (host) "
+              f"{r['rcm_order_ms']:.1f} ms, permute {r['permute_ms']:.1f} ms; bandwidth max/avg {r['bandwidth_before'][0]}/"
+              f"{r['bandwidth_before'][1]:.0f} -> {r['bandwidth_after'][0]}/{r['bandwidth_after'][1]:.0f}; "
+              f"A^2 {r['a2_ms']:.3f} -> {r['a2_rcm_ms']:.3f} ms; exact {r.get('from_edges_exact', '-')}, "
+              f"same order {r.get('rcm_order_equal', '-')}")
     for g in out.get("generators", []):
         print(f"\n{g['cell']}: host library {g['host_ms']:.1f} ms, device {g['device_ms']:.1f} ms, identical {g['identical']}")
 
