@@ -22,6 +22,7 @@
  *   CsrMatrix::permute / unpermute src/graph_csr.rs:726-799  slat_csr_permute
  *   CsrMatrix::bandwidth_stats src/graph_csr.rs:802-818      slat_bandwidth_stats
  *   load_edges (tests)      src/graph_csr.rs:1209-1224       slat_load_edges
+ *   einsum_sparse_driven    einsum-dyn/src/sparse.rs:70-148  slat_spgemm_dense
  *   assert_eq!(self.n, other.n) panics (graph_csr.rs:307,351)  -> SLAT_EDIM
  *
  * Conventions:
@@ -231,6 +232,15 @@ slat_status slat_csr_permute(slat_ctx *ctx, const slat_csr_view *m, const uint32
                              slat_csr *out);
 /* CsrMatrix::bandwidth_stats (src/graph_csr.rs:802-818): max |r-c| and mean |r-c| over entries. */
 slat_status slat_bandwidth_stats(slat_ctx *ctx, const slat_csr_view *m, uint64_t *max_bw, double *avg_bw);
+
+/* --- sparse x sparse with a dense output ---------------------------- */
+/* einsum_sparse_driven (einsum-dyn/src/sparse.rs:70-148), "ab,bc->ac" (transpose = 0) or
+ * "ab,bc->ca" (1): every output entry that some product touches is overwritten with its sum,
+ * untouched entries keep their content. `out` is row-major with leading dimension ld, device or
+ * host memory per out_residency. Values: SLAT_U32 as plain u32 (wrapping `+=` and `*`, the einsum
+ * tests' T) or SLAT_F64 (the reference's left fold, bit-exact); SLAT_SAT64 -> SLAT_ENOTSUP. */
+slat_status slat_spgemm_dense(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, void *out, uint64_t ld,
+                              int32_t transpose, int32_t out_residency);
 
 
 #ifdef __cplusplus

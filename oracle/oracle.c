@@ -937,3 +937,42 @@ done:
     *dst = d;
     return 0;
 }
+
+/* einsum_sparse_driven (einsum-dyn/src/sparse.rs:70-148), "ab,bc->ac" (trans 0) or "->ca" (1):
+ * a dense accumulator per A row, touched columns listed when their accumulator reads 0, written
+ * out and cleared. u32 = plain wrapping u32 (the einsum tests' T); f64 = the same left fold. */
+int orc_einsum_sparse_driven(const orc_csr *a, const orc_csr *b, void *out, uint64_t ld, int trans) {
+    if (a->dtype != b->dtype || a->dtype == ORC_SAT64) return -1;
+    const uint64_t m = b->n;
+    const int f = a->dtype == ORC_F64;
+    double *accd = calloc(m ? m : 1, 8);
+    uint32_t *accu = calloc(m ? m : 1, 4);
+    uint64_t *nz = malloc((m ? m : 1) * 8 * 4 + 64), nzcap = (m ? m : 1) * 4, nn = 0;
+    for (uint64_t i = 0; i < a->n; ++i) {
+        nn = 0;
+        for (uint64_t e = a->row_ptr[i]; e < a->row_ptr[i + 1]; ++e) {
+            const uint64_t k = a->col[e];
+            for (uint64_t t = b->row_ptr[k]; t < b->row_ptr[k + 1]; ++t) {
+                const uint64_t j = b->col[t];
+                const int zero = f ? accd[j] == 0.0 : accu[j] == 0;
+                if (zero) {
+                    if (nn == nzcap) { nzcap *= 2; nz = realloc(nz, nzcap * 8); }
+                    nz[nn++] = j;
+                }
+                if (f) {
+                    volatile double p = ((const double *)a->val)[e] * ((const double *)b->val)[t];
+                    accd[j] = accd[j] + p;
+                } else {
+                    accu[j] += ((const uint32_t *)a->val)[e] * ((const uint32_t *)b->val)[t];
+                }
+            }
+        }
+        for (uint64_t q = 0; q < nn; ++q) {
+            const uint64_t j = nz[q], at = trans ? j * ld + i : i * ld + j;
+            if (f) { ((double *)out)[at] = accd[j]; accd[j] = 0.0; }
+            else { ((uint32_t *)out)[at] = accu[j]; accu[j] = 0; }
+        }
+    }
+    free(accd); free(accu); free(nz);
+    return 0;
+}

@@ -27,6 +27,7 @@
  *   orc_permute      CsrMatrix::permute          src/graph_csr.rs:726-783 (perm[new] = old)
  *   orc_bandwidth_stats CsrMatrix::bandwidth_stats src/graph_csr.rs:802-818
  *   orc_load_edges   load_edges                  src/graph_csr.rs:1209-1224
+ *   orc_einsum_sparse_driven einsum_sparse_driven einsum-dyn/src/sparse.rs:70-148 (dense output)
  *
  * Parity pin: see tests/golden/ (nnz sequence that rounds to README.md:41-46, SHA-256 of the
  * arrays computed independently by tests/golden/make_golden.py with numpy+scipy).
@@ -83,6 +84,7 @@ int orc_rcm_order(const orc_csr *a, uint32_t *perm);
 int orc_permute(const orc_csr *a, const uint32_t *perm, orc_csr *out);
 void orc_bandwidth_stats(const orc_csr *a, uint64_t *max_bw, double *avg_bw);
 /* "<a> <b>" per non-empty line; n = max id + 1; src and dst arrays malloc-ed. -1 on a malformed line. */
+int orc_einsum_sparse_driven(const orc_csr *a, const orc_csr *b, void *out, uint64_t ld, int trans);
 int orc_load_edges(const char *path, uint64_t *n, uint64_t *n_edges, uint32_t **src, uint32_t **dst);
 
 #ifdef __cplusplus

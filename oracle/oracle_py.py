@@ -67,6 +67,7 @@ def lib():
         L.orc_reachability_sum.argtypes = [P(_Csr), P(C.c_uint64), P(_Csr)]
         L.orc_connected_components.argtypes = [P(_Csr), C.c_void_p]
         L.orc_rcm_order.argtypes = [P(_Csr), C.c_void_p]
+        L.orc_einsum_sparse_driven.argtypes = [P(_Csr), P(_Csr), C.c_void_p, C.c_uint64, C.c_int]
         L.orc_permute.argtypes = [P(_Csr), C.c_void_p, P(_Csr)]
         L.orc_bandwidth_stats.argtypes = [P(_Csr), P(C.c_uint64), P(C.c_double)]
         L.orc_load_edges.argtypes = [C.c_char_p, P(C.c_uint64), P(C.c_uint64), P(C.c_void_p), P(C.c_void_p)]
@@ -239,6 +240,15 @@ def bandwidth_stats(a: Csr):
     mx, avg = C.c_uint64(), C.c_double()
     lib().orc_bandwidth_stats(C.byref(a._raw), C.byref(mx), C.byref(avg))
     return int(mx.value), float(avg.value)
+
+
+def einsum_sparse_driven(a: Csr, b: Csr, out: np.ndarray, transpose: bool = False) -> np.ndarray:
+    """einsum_sparse_driven (einsum-dyn/src/sparse.rs:70-148) into the dense array `out` (touched
+    entries overwritten, the rest kept)."""
+    if lib().orc_einsum_sparse_driven(C.byref(a._raw), C.byref(b._raw), out.ctypes.data, out.shape[1],
+                                      int(transpose)) != 0:
+        raise ValueError("einsum_sparse_driven: u32 or f64 operands of one type")
+    return out
 
 
 def load_edges(path: str):

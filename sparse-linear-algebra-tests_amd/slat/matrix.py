@@ -355,6 +355,22 @@ class DeviceCsr:
         L.check(L.lib().slat_bandwidth_stats(self._ctx.ptr, C.byref(v), C.byref(mx), C.byref(avg)), self._ctx.ptr)
         return int(mx.value), float(avg.value)
 
+    # -- dense output (einsum-dyn/src/sparse.rs:70-148) ---------------------------------------------
+    def einsum_sparse_driven(self, other: "DeviceCsr", out: np.ndarray | None = None, transpose: bool = False):
+        """einsum_sparse_driven("ab,bc->ac" | "ab,bc->ca", self, other, out): touched entries of the
+        dense host array `out` are overwritten with their sums, the rest kept. u32 values are plain
+        (wrapping) u32 here, as in the einsum tests; f64 folds like the reference."""
+        rows, cols = (other.n, self.n) if transpose else (self.n, other.n)
+        dt = np.uint32 if self.DTYPE == L.U32 else np.float64
+        if out is None:
+            out = np.zeros((rows, cols), dt)
+        if out.dtype != dt or out.ndim != 2 or out.shape[0] != rows or out.shape[1] < cols or not out.flags.c_contiguous:
+            raise ValueError("out: C-contiguous (rows, >= cols) array of the value type")
+        a, b = self.view(), other.view()
+        L.check(L.lib().slat_spgemm_dense(self._ctx.ptr, C.byref(a), C.byref(b), out.ctypes.data, out.shape[1],
+                                          int(transpose), L.HOST), self._ctx.ptr)
+        return out
+
     # -- accessors ---------------------------------------------------------------------------------
     @property
     def n(self) -> int:
