@@ -241,6 +241,11 @@ slat_status slat_bandwidth_stats(slat_ctx *ctx, const slat_csr_view *m, uint64_t
  * tests' T) or SLAT_F64 (the reference's left fold, bit-exact); SLAT_SAT64 -> SLAT_ENOTSUP. */
 slat_status slat_spgemm_dense(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, void *out, uint64_t ld,
                               int32_t transpose, int32_t out_residency);
+/* Device buffers for dense operands (the context's block cache) and host <-> device copies
+ * (to_host = 1: device src -> host dst; 0: host src -> device dst), synchronous. */
+slat_status slat_device_alloc(slat_ctx *ctx, uint64_t bytes, void **p);
+slat_status slat_device_free(slat_ctx *ctx, void *p);
+slat_status slat_device_copy(slat_ctx *ctx, void *dst, const void *src, uint64_t bytes, int32_t to_host);
 
 
 #ifdef __cplusplus

@@ -98,3 +98,25 @@ extern "C" slat_status slat_spgemm_dense(slat_ctx *ctx, const slat_csr_view *A, 
     SLAT_HIP(ctx, hipStreamSynchronize(s));
     return SLAT_OK;
 }
+
+// device buffers for dense operands (from the context's block cache) and their host copies
+extern "C" slat_status slat_device_alloc(slat_ctx *ctx, uint64_t bytes, void **p) {
+    if (!ctx || !p) return SLAT_EINVAL;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    if (slat_dev_alloc(ctx, p, bytes, ctx->stream) != hipSuccess) return fail(ctx, SLAT_EOOM, "device buffer");
+    return SLAT_OK;
+}
+extern "C" slat_status slat_device_free(slat_ctx *ctx, void *p) {
+    if (!ctx) return SLAT_EINVAL;
+    if (p) slat_dev_free(ctx, p, ctx->stream);
+    return SLAT_OK;
+}
+extern "C" slat_status slat_device_copy(slat_ctx *ctx, void *dst, const void *src, uint64_t bytes, int32_t to_host) {
+    if (!ctx || (bytes && (!dst || !src))) return SLAT_EINVAL;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    if (bytes)
+        SLAT_HIP(ctx, hipMemcpyAsync(dst, src, bytes, to_host ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice,
+                                     ctx->stream));
+    SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SLAT_OK;
+}

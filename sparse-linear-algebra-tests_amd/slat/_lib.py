@@ -25,7 +25,7 @@ EXPORTS = [
     "slat_csr_add", "slat_csr_identity", "slat_csr_pattern_equal", "slat_reachability_sum",
     "slat_power_until_stable", "slat_connected_components", "slat_csr_from_coo", "slat_csr_lattice", "slat_csr_thin",
     "slat_load_edges", "slat_edges_free", "slat_csr_from_edges", "slat_rcm_order", "slat_csr_permute",
-    "slat_bandwidth_stats", "slat_spgemm_dense",
+    "slat_bandwidth_stats", "slat_spgemm_dense", "slat_device_alloc", "slat_device_free", "slat_device_copy",
 ]
 
 
@@ -128,6 +128,9 @@ def lib():
         "slat_csr_permute": ([vp, P(CsrView), vp, i32, P(CsrOwned)], C.c_int),
         "slat_bandwidth_stats": ([vp, P(CsrView), P(u64), P(C.c_double)], C.c_int),
         "slat_spgemm_dense": ([vp, P(CsrView), P(CsrView), vp, u64, i32, i32], C.c_int),
+        "slat_device_alloc": ([vp, u64, P(vp)], C.c_int),
+        "slat_device_free": ([vp, vp], C.c_int),
+        "slat_device_copy": ([vp, vp, vp, u64, i32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

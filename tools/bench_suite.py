@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=2.0, help="seconds of timed CPU calls per cell")
     ap.add_argument("--cpu-max-nnz", type=float, default=3e7, help="skip the CPU leg above this nnz(A)")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
-    ap.add_argument("--only", default="GEN,C1,C2,C3,C4,C5,RG")
+    ap.add_argument("--only", default="GEN,C1,C2,C3,C4,C5,RG,DN")
     ap.add_argument("--rmat-scale", type=int, default=16)
     ap.add_argument("--rmat-deg", type=int, default=16)
     args = ap.parse_args()
@@ -214,6 +214,45 @@ def main():
             out["cells"] += [c0, c1]
             print(json.dumps(rec), file=sys.stderr, flush=True)
             out.setdefault("real_graph", []).append(rec)
+    if "DN" in only:
+        # einsum_sparse_driven (einsum-dyn/src/sparse.rs:70-148): sparse x sparse into a dense
+        # output resident on the device (a library buffer), checked against the oracle
+        Cc = slat._lib.C
+        oA = O.torus_thinned(30, 3.0, O.Rng())
+        dA = to_dev(oA, M, ctx)
+        oP = O.matmul_seq(O.matmul_seq(oA, oA), oA)
+        dP = to_dev(oP, M, ctx)
+        h = slat.host_rmat(14, (1 << 14) * 16)
+        oR = O.from_arrays(h.row_ptr, h.col_idx, h.values, O.F64)
+        dR = slat.CsrF64.from_host(h, ctx)
+        for name, da, db, oa, ob, ndt in [("torus30 A*A u32", dA, dA, oA, oA, np.uint32),
+                                          ("torus30 A^3*A u32", dP, dA, oP, oA, np.uint32),
+                                          ("rmat14 A*A f64", dR, dR, oR, oR, np.float64)]:
+            n = oa.n
+            got = np.zeros((n, n), ndt)
+            buf = Cc.c_void_p()
+            slat.lib().slat_device_alloc(ctx.ptr, got.nbytes, Cc.byref(buf))
+            slat.lib().slat_device_copy(ctx.ptr, buf, got.ctypes.data, got.nbytes, 0)
+
+            def call():
+                va, vb = da.view(), db.view()
+                rc = slat.lib().slat_spgemm_dense(ctx.ptr, Cc.byref(va), Cc.byref(vb), buf, n, 0, slat.DEVICE)
+                assert rc == 0
+            call()
+            t = gpu_time(call)
+            slat.lib().slat_device_copy(ctx.ptr, got.ctypes.data, buf, got.nbytes, 1)
+            slat.lib().slat_device_free(ctx.ptr, buf)
+            want = O.einsum_sparse_driven(oa, ob, np.zeros((n, n), ndt))
+            same_ = bool(np.array_equal(got.view(np.uint64) if ndt == np.float64 else got,
+                                        want.view(np.uint64) if ndt == np.float64 else want))
+            products = O.flops(oa, ob)
+            rec = {"cell": f"DN {name}", "n": n, "gpu_ms": t * 1e3, "products": products,
+                   "gprod_s": products / t / 1e9, "bit_exact": same_}
+            if args.cpu:
+                tc = cpu_time(lambda: O.einsum_sparse_driven(oa, ob, np.zeros((n, n), ndt)), args.cpu_budget, 3)
+                rec.update({"cpu_1thr_ms": tc * 1e3, "speedup": tc / t})
+            print(json.dumps(rec), file=sys.stderr, flush=True)
+            out.setdefault("dense_out", []).append(rec)
 
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, "w") as f:
@@ -232,6 +271,9 @@ def main():
               f"{r['bandwidth_before'][1]:.0f} -> {r['bandwidth_after'][0]}/{r['bandwidth_after'][1]:.0f}; "
               f"A^2 {r['a2_ms']:.3f} -> {r['a2_rcm_ms']:.3f} ms; exact {r.get('from_edges_exact', '-')}, "
               f"same order {r.get('rcm_order_equal', '-')}")
+    for r in out.get("dense_out", []):
+        print(f"\n{r['cell']}: GPU {r['gpu_ms']:.3f} ms ({r['gprod_s']:.2f} G products/s), "
+              f"oracle 1 thread {r.get('cpu_1thr_ms', float('nan')):.1f} ms, bit-exact {r['bit_exact']}")
     for g in out.get("generators", []):
         print(f"\n{g['cell']}: host library {g['host_ms']:.1f} ms, device {g['device_ms']:.1f} ms, identical {g['identical']}")
 
