@@ -12,6 +12,7 @@
  *   CsrMatrix::from_coo     src/graph_csr.rs:83-129          slat_csr_from_coo (device) / slat_host_from_coo
  *   CsrMatrix::lattice      src/graph_csr.rs:177-222         slat_csr_lattice (device) / slat_host_lattice
  *   CsrMatrix::thin         src/graph_csr.rs:225-247         slat_csr_thin (device) / slat_host_thin
+ *   CsrMatrix::random       src/graph_csr.rs:163-174         slat_host_random
  *   CsrMatrix::add          src/graph_csr.rs:487-542         slat_csr_add
  *   CsrMatrix::identity     src/graph_csr.rs:68-80           slat_csr_identity
  *   CsrMatrix::reachability_sum    src/graph_csr.rs:545-559  slat_reachability_sum
@@ -181,6 +182,9 @@ typedef struct { uint8_t opaque[512]; } slat_rng; /* rand 0.9 StdRng (ChaCha12) 
 
 void slat_rng_seed(slat_rng *rng, const uint8_t seed[32]);
 uint64_t slat_rng_next_u64(slat_rng *rng);
+uint32_t slat_rng_next_u32(slat_rng *rng);
+/* rand 0.9 `rng.random_range(lo..hi)` for usize / u32 bounds below 2^32 (lo < hi). */
+uint32_t slat_rng_range_u32(slat_rng *rng, uint32_t lo, uint32_t hi);
 double slat_rng_next_f64(slat_rng *rng);
 /* CsrMatrix::from_coo (src/graph_csr.rs:83-129): sort, merge duplicates by summing, drop zeros. */
 slat_status slat_host_from_coo(uint64_t n, uint64_t ntrip, const uint32_t *rows, const uint32_t *cols,
@@ -189,6 +193,9 @@ slat_status slat_host_from_coo(uint64_t n, uint64_t ntrip, const uint32_t *rows,
 slat_status slat_host_lattice(const uint64_t *dims, int ndim, int torus, slat_host_csr *out);
 /* CsrMatrix::thin (src/graph_csr.rs:225-247). */
 slat_status slat_host_thin(const slat_host_csr *m, slat_rng *rng, double density, slat_host_csr *out);
+/* CsrMatrix::random (src/graph_csr.rs:163-174): random directed graph, n >= 2 nodes, m edge draws
+ * without self-loops, duplicates summed (u32 values). */
+slat_status slat_host_random(slat_rng *rng, uint32_t n, uint64_t m, slat_host_csr *out);
 /* Seeded R-MAT power-law graph with f64 values uniform in [0.5, 1.5) (config C5; not in the
  * reference, which has no power-law generator). */
 slat_status slat_host_rmat(uint32_t scale, uint64_t n_edges, double a, double b, double c,

@@ -60,11 +60,42 @@ static void orc_rng_refill(orc_rng *r) {
     r->idx = 0;
 }
 
+/* rand_core 0.9 BlockRng::next_u64: two consecutive words; at the last word of the buffer the
+ * low half is that word and the high half the first word of the next refill. */
 uint64_t orc_rng_next_u64(orc_rng *r) {
     if (r->idx >= 64) orc_rng_refill(r);
+    if (r->idx == 63) {
+        const uint64_t lo = r->buf[63];
+        orc_rng_refill(r);
+        r->idx = 1;
+        return lo | ((uint64_t)r->buf[0] << 32);
+    }
     uint64_t lo = r->buf[r->idx], hi = r->buf[r->idx + 1];
     r->idx += 2;
     return lo | (hi << 32);
+}
+
+/* rand_core 0.9 BlockRng::next_u32: one word. */
+uint32_t orc_rng_next_u32(orc_rng *r) {
+    if (r->idx >= 64) orc_rng_refill(r);
+    return r->buf[r->idx++];
+}
+
+/* rand 0.9 `random_range(lo..hi)` for usize / u32 with hi <= u32::MAX: UniformUsize samples as
+ * u32 (portable across pointer widths), UniformInt<u32>::sample_single_inclusive(lo, hi - 1) by
+ * Canon's method — one u32 draw widened-multiplied by the range; only when the low half exceeds
+ * 2^32 - range a second draw's high half is added to it, and its carry bumps the result. */
+uint32_t orc_rng_range_u32(orc_rng *r, uint32_t lo, uint32_t hi) {
+    const uint32_t range = hi - lo; /* (hi - 1) - lo + 1; 0 = the full u32 range */
+    if (range == 0) return orc_rng_next_u32(r);
+    const uint64_t m = (uint64_t)orc_rng_next_u32(r) * range;
+    uint32_t result = (uint32_t)(m >> 32);
+    const uint32_t lo_order = (uint32_t)m;
+    if (lo_order > (uint32_t)(0u - range)) {
+        const uint32_t new_hi = (uint32_t)(((uint64_t)orc_rng_next_u32(r) * range) >> 32);
+        if ((uint32_t)(lo_order + new_hi) < lo_order) result += 1;
+    }
+    return lo + result;
 }
 
 /* rand 0.9 `random_range(0.0..1.0)` for f64: value1_2 - 1.0 with 52 random mantissa bits. */
@@ -258,6 +289,24 @@ int orc_thin(const orc_csr *m, orc_rng *rng, double density, orc_csr *out) {
         }
     }
     int rc = from_trips(m->n, t, nt, m->dtype, out);
+    free(t);
+    return rc;
+}
+
+/* CsrMatrix::random (src/graph_csr.rs:163-174): m draws of r in 0..n, c in 0..n-1 bumped past r
+ * (no self-loops), value 1, then from_coo (duplicates summed). u32 values. */
+int orc_random(orc_rng *rng, uint32_t n, uint64_t m, orc_csr *out) {
+    if (n < 2) return -1; /* assert!(nu >= 2) */
+    trip *t = (trip *)malloc((m ? m : 1) * sizeof(trip));
+    if (!t) return -1;
+    for (uint64_t i = 0; i < m; ++i) {
+        const uint32_t r = orc_rng_range_u32(rng, 0, n);
+        uint32_t c = orc_rng_range_u32(rng, 0, n - 1);
+        if (c >= r) c += 1;
+        t[i].key = ((uint64_t)r << 32) | c;
+        t[i].v = 1;
+    }
+    int rc = from_trips(n, t, m, ORC_U32, out);
     free(t);
     return rc;
 }

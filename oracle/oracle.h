@@ -11,6 +11,12 @@
  *   orc_lattice      CsrMatrix::lattice          src/graph_csr.rs:177-222
  *   orc_thin         CsrMatrix::thin             src/graph_csr.rs:225-247 (same draw pattern as
  *                    SparseCountMatrix::thin, src/graph.rs:143-154)
+ *   orc_random       CsrMatrix::random           src/graph_csr.rs:163-174; integer draws as rand 0.9's
+ *                    `random_range(0..n)` for usize: UniformUsize -> UniformInt<u32> (n <= u32::MAX),
+ *                    Canon's method on next_u32 words (rand_core BlockRng word order). Pinned by the
+ *                    nnz the reference's einsum study prints for random(1000, 5000) / (2000, 10000)
+ *                    after three 4/26 thins from seed [42;32] (SPARSE_EINSUM_APPROACHES.md:127-132,
+ *                    configs src/graph_csr.rs:1652-1669).
  *   orc_from_coo     CsrMatrix::from_coo         src/graph_csr.rs:83-129
  *   orc_matmul_seq   CsrMatrix::matmul           src/graph_csr.rs:306-346   (u32 saturating)
  *                    same algorithm on Sat64     src/graph_sprs.rs:15-86    (u64 saturating)
@@ -61,7 +67,10 @@ typedef struct {
 
 void orc_rng_seed(orc_rng *r, const uint8_t seed[32]);
 uint64_t orc_rng_next_u64(orc_rng *r);
+uint32_t orc_rng_next_u32(orc_rng *r);
+uint32_t orc_rng_range_u32(orc_rng *r, uint32_t lo, uint32_t hi);
 double orc_rng_next_f64(orc_rng *r);
+int orc_random(orc_rng *rng, uint32_t n, uint64_t m, orc_csr *out);
 void orc_chacha12_block(const uint32_t key[8], uint64_t counter, uint32_t out[16]);
 
 void orc_csr_free(orc_csr *m);

@@ -50,6 +50,11 @@ def lib():
         L.orc_rng_next_u64.restype = C.c_uint64
         L.orc_rng_next_f64.argtypes = [P(_Rng)]
         L.orc_rng_next_f64.restype = C.c_double
+        L.orc_rng_next_u32.argtypes = [P(_Rng)]
+        L.orc_rng_next_u32.restype = C.c_uint32
+        L.orc_rng_range_u32.argtypes = [P(_Rng), C.c_uint32, C.c_uint32]
+        L.orc_rng_range_u32.restype = C.c_uint32
+        L.orc_random.argtypes = [P(_Rng), C.c_uint32, C.c_uint64, P(_Csr)]
         L.orc_chacha12_block.argtypes = [P(C.c_uint32), C.c_uint64, P(C.c_uint32)]
         L.orc_csr_free.argtypes = [P(_Csr)]
         L.orc_from_coo.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
@@ -88,6 +93,13 @@ class Rng:
 
     def next_f64(self) -> float:
         return lib().orc_rng_next_f64(C.byref(self._r))
+
+    def next_u32(self) -> int:
+        return lib().orc_rng_next_u32(C.byref(self._r))
+
+    def range_u32(self, lo: int, hi: int) -> int:
+        """rand 0.9 `random_range(lo..hi)` for usize / u32 (Canon's method on u32 draws)."""
+        return lib().orc_rng_range_u32(C.byref(self._r), lo, hi)
 
 
 class Csr:
@@ -170,6 +182,11 @@ def lattice(dims, torus: bool) -> Csr:
 
 def thin(m: Csr, rng: Rng, density: float) -> Csr:
     return _new(lib().orc_thin, C.byref(m._raw), C.byref(rng._r), density)
+
+
+def random(rng: Rng, n: int, m: int) -> Csr:
+    """CsrMatrix::random (src/graph_csr.rs:163-174)."""
+    return _new(lib().orc_random, C.byref(rng._r), n, m)
 
 
 def convert(m: Csr, dtype: int) -> Csr:

@@ -7,6 +7,8 @@
 //                       column sort, duplicates summed, zeros dropped)
 //   slat_host_lattice   CsrMatrix::lattice    src/graph_csr.rs:177-222
 //   slat_host_thin      CsrMatrix::thin       src/graph_csr.rs:225-247
+//   slat_host_random    CsrMatrix::random     src/graph_csr.rs:163-174 (rand 0.9 integer
+//                       random_range: UniformUsize -> u32 Canon's method, BlockRng word order)
 //   slat_host_rmat      seeded R-MAT for the f64 power-law config (not in the reference)
 #include <algorithm>
 #include <cstdio>
@@ -146,16 +148,49 @@ void slat_rng_seed(slat_rng *rng, const uint8_t seed[32]) {
     r->idx = 64;
 }
 
+static void refill(Rng *r) {
+    for (int b = 0; b < 4; ++b) chacha12(r->key, r->counter + (uint64_t)b, r->buf + 16 * b);
+    r->counter += 4;
+    r->idx = 0;
+}
+
+// rand_core 0.9 BlockRng::next_u64: two consecutive words; from the buffer's last word, the low
+// half is that word and the high half the first word of the next refill
 uint64_t slat_rng_next_u64(slat_rng *rng) {
     Rng *r = R(rng);
-    if (r->idx >= 64) {  // only u64 draws on this path: idx stays even
-        for (int b = 0; b < 4; ++b) chacha12(r->key, r->counter + (uint64_t)b, r->buf + 16 * b);
-        r->counter += 4;
-        r->idx = 0;
+    if (r->idx >= 64) refill(r);
+    if (r->idx == 63) {
+        const uint64_t lo = r->buf[63];
+        refill(r);
+        r->idx = 1;
+        return lo | ((uint64_t)r->buf[0] << 32);
     }
     const uint64_t lo = r->buf[r->idx], hi = r->buf[r->idx + 1];
     r->idx += 2;
     return lo | (hi << 32);
+}
+
+// rand_core 0.9 BlockRng::next_u32: one word
+uint32_t slat_rng_next_u32(slat_rng *rng) {
+    Rng *r = R(rng);
+    if (r->idx >= 64) refill(r);
+    return r->buf[r->idx++];
+}
+
+// rand 0.9 `random_range(lo..hi)` for usize / u32 with hi <= u32::MAX: UniformUsize samples as u32,
+// UniformInt<u32>::sample_single_inclusive(lo, hi - 1) by Canon's method (a second draw only when
+// the low half of the first product exceeds 2^32 - range; its carry bumps the result)
+uint32_t slat_rng_range_u32(slat_rng *rng, uint32_t lo, uint32_t hi) {
+    const uint32_t range = hi - lo;  // 0 = the whole u32 range
+    if (range == 0) return slat_rng_next_u32(rng);
+    const uint64_t m = (uint64_t)slat_rng_next_u32(rng) * range;
+    uint32_t result = (uint32_t)(m >> 32);
+    const uint32_t lo_order = (uint32_t)m;
+    if (lo_order > 0u - range) {
+        const uint32_t new_hi = (uint32_t)(((uint64_t)slat_rng_next_u32(rng) * range) >> 32);
+        if ((uint32_t)(lo_order + new_hi) < lo_order) result += 1;
+    }
+    return lo + result;
 }
 
 double slat_rng_next_f64(slat_rng *rng) {
@@ -176,7 +211,7 @@ void slat_rng_advance(slat_rng *rng, uint64_t draws) {
     uint32_t key[8];
     uint64_t w;
     slat_rng_position(rng, key, &w);
-    w += 2 * draws;
+    w += 2 * draws;  // f64 draws: two words each
     r->counter = (w / 64) * 4;
     r->idx = 64;
     if (w % 64) {  // mid-refill: the 4 blocks holding word w, read position inside them
@@ -274,6 +309,20 @@ slat_status slat_host_thin(const slat_host_csr *m, slat_rng *rng, double density
         }
     }
     return build(m->n, t, m->dtype, out);
+}
+
+// CsrMatrix::random (src/graph_csr.rs:163-174): m edges r in 0..n, c in 0..n-1 bumped past r (no
+// self-loops), value 1, duplicates summed by from_coo
+slat_status slat_host_random(slat_rng *rng, uint32_t n, uint64_t m, slat_host_csr *out) {
+    if (!rng || !out || n < 2) return SLAT_EINVAL;  // assert!(nu >= 2)
+    std::vector<Trip> t(m);
+    for (uint64_t i = 0; i < m; ++i) {
+        const uint32_t r = slat_rng_range_u32(rng, 0, n);
+        uint32_t c = slat_rng_range_u32(rng, 0, n - 1);
+        if (c >= r) c += 1;
+        t[i] = {r, c, 1};
+    }
+    return build(n, t, SLAT_U32, out);
 }
 
 slat_status slat_host_rmat(uint32_t scale, uint64_t n_edges, double a, double b, double c, const uint8_t seed[32],

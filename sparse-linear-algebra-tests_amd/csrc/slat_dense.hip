@@ -1,11 +1,21 @@
 // slat_dense.hip — sparse x sparse with a dense output: the Sparse2D
 // driver einsum_sparse_driven (einsum-dyn/src/sparse.rs:70-148), spec "ab,bc->ac" (or "->ca").
-// The reference keeps a dense row accumulator and writes every touched column of the output row,
-// leaving untouched entries as they were. Here one wavefront owns an output row: pass 1 stores 0
-// at every touched column, pass 2 adds the products in place. Integer T (plain u32: the einsum
-// tests' T, wrapping `+=` / `*` of a release build) adds with atomics, since wrapping sums are
-// order-free. f64 keeps the reference's left fold: the A entries of the row in order, each a
-// read-modify-write of distinct columns (one B row), the next step issued after the stores land.
+//
+// The reference keeps a dense row accumulator `acc` and lists column j in `nz_cols` every time
+// acc[j] reads T::default() before an add (sparse.rs:126-129); afterwards it writes acc[j] and
+// clears it once per listing, in listing order (:137-143). A column listed once ends at its sum
+// (0 + p1 + p2 + ... in visiting order); a column listed again — its running sum passed through 0
+// after the first add: a u32 product that wraps to 0, an exact f64 cancellation — is written a
+// second time after the clear, so it ends at 0. Untouched columns keep their content.
+//
+// Here one wavefront owns an output row and walks its products in the reference's order (A row
+// entries ascending, then each B row; the lanes spread over one B row, whose columns are
+// distinct). Per column window it keeps two LDS bitmaps: `seen` (touched before in this row) and
+// `dead` (listed twice: the output is 0, later adds change nothing). A first touch stores 0 + p;
+// a later touch reads the running sum from the output, marks the column dead if it is 0 (and
+// stores 0), else stores sum + p. The next A entry waits for these stores (it may hit the same
+// columns). T is plain u32 (the einsum tests' T, wrapping `+=` / `*` of a release build) or f64
+// (`__dmul_rn` / `__dadd_rn`, no FMA: Rust never fuses).
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -15,41 +25,75 @@
 
 namespace {
 
-constexpr int kB = 256, kW = 64;
+constexpr int kB = 256, kW = 64, kWpb = kB / kW;
+constexpr uint32_t kMaxWinBits = 1u << 16;  // columns per window (2 x 8 KB of bitmaps per wave)
 
-template <typename T, bool ORDERED>
+template <typename T>
+__device__ __forceinline__ T dmul(T a, T b) {
+    if constexpr (sizeof(T) == 8) return __dmul_rn(a, b); else return a * b;
+}
+template <typename T>
+__device__ __forceinline__ T dadd(T a, T b) {
+    if constexpr (sizeof(T) == 8) return __dadd_rn(a, b); else return a + b;
+}
+
+template <typename T>
 __global__ __launch_bounds__(kB) void k_dense_out(const uint64_t *arp, const uint32_t *acol, const T *aval,
                                                   const uint64_t *brp, const uint32_t *bcol, const T *bval,
-                                                  uint64_t nrows, uint64_t bn, T *out, uint64_t ld, int trans) {
+                                                  uint64_t nrows, uint64_t bn, uint64_t ncols, uint32_t win,
+                                                  T *out, uint64_t ld, int trans) {
+    extern __shared__ uint32_t sm[];
     const int lane = threadIdx.x & (kW - 1);
-    const uint64_t waves = (uint64_t)gridDim.x * (kB / kW);
-    for (uint64_t i = (uint64_t)blockIdx.x * (kB / kW) + threadIdx.x / kW; i < nrows; i += waves) {
+    const uint32_t words = win / 32;
+    uint32_t *seen = sm + (threadIdx.x / kW) * 2 * words, *dead = seen + words;
+    for (uint32_t w = lane; w < 2 * words; w += kW) seen[w] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t waves = (uint64_t)gridDim.x * kWpb;
+    for (uint64_t i = (uint64_t)blockIdx.x * kWpb + threadIdx.x / kW; i < nrows; i += waves) {
         const uint64_t a0 = arp[i], a1 = arp[i + 1];
         auto at = [&](uint32_t j) -> T * { return trans ? out + (uint64_t)j * ld + i : out + i * ld + j; };
-        // pass 1: the touched columns start from T::default()
-        for (uint64_t e = a0; e < a1; ++e) {
-            const uint32_t k = acol[e];
-            if (k >= bn) continue;  // malformed input: no such B row
-            for (uint64_t t = brp[k] + lane; t < brp[k + 1]; t += kW) *at(bcol[t]) = T(0);
-        }
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        // pass 2: acc[j] += a * b in A-row order, then B-row order
-        for (uint64_t e = a0; e < a1; ++e) {
-            const uint32_t k = acol[e];
-            if (k >= bn) continue;
-            const T a = aval[e];
-            for (uint64_t t = brp[k] + lane; t < brp[k + 1]; t += kW) {
-                T *p = at(bcol[t]);
-                if constexpr (ORDERED) {
-                    const T v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(p, __dadd_rn(v, __dmul_rn(a, bval[t])), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    atomicAdd(p, (T)(a * bval[t]));
+        for (uint64_t wlo = 0; wlo < ncols; wlo += win) {
+            for (uint64_t e = a0; e < a1; ++e) {
+                const uint32_t k = acol[e];
+                if (k >= bn) continue;  // malformed input: no such B row
+                const T a = aval[e];
+                for (uint64_t t = brp[k] + lane; t < brp[k + 1]; t += kW) {
+                    const uint32_t j = bcol[t];
+                    const uint64_t off = (uint64_t)j - wlo;
+                    if (off >= win) continue;
+                    const uint32_t w = (uint32_t)off >> 5, bit = 1u << (off & 31);
+                    const T p = dmul(a, bval[t]);
+                    T *q = at(j);
+                    if (!(seen[w] & bit)) {
+                        __hip_atomic_store(q, dadd(T(0), p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        atomicOr(&seen[w], bit);
+                    } else if (!(dead[w] & bit)) {
+                        const T v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (v == T(0)) {  // listed again: the second write (of 0) wins
+                            __hip_atomic_store(q, T(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            atomicOr(&dead[w], bit);
+                        } else {
+                            __hip_atomic_store(q, dadd(v, p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0);  // the next entry may hit these columns (stores and bits)
+                __builtin_amdgcn_wave_barrier();
+            }
+            // clear the bits this row set (the same walk)
+            for (uint64_t e = a0; e < a1; ++e) {
+                const uint32_t k = acol[e];
+                if (k >= bn) continue;
+                for (uint64_t t = brp[k] + lane; t < brp[k + 1]; t += kW) {
+                    const uint64_t off = (uint64_t)bcol[t] - wlo;
+                    if (off < win) {
+                        seen[off >> 5] = 0;
+                        dead[off >> 5] = 0;
+                    }
                 }
             }
-            if constexpr (ORDERED) __builtin_amdgcn_s_waitcnt(0);  // the next entry may hit these columns
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
         }
     }
 }
@@ -76,16 +120,20 @@ extern "C" slat_status slat_spgemm_dense(slat_ctx *ctx, const slat_csr_view *A, 
         SLAT_HIP(ctx, slat_dev_alloc(ctx, &dout, bytes, s));
         SLAT_HIP(ctx, hipMemcpyAsync(dout, out, bytes, hipMemcpyHostToDevice, s));
     }
-    if (A->n_rows) {
-        const unsigned g = (unsigned)std::min<uint64_t>((A->n_rows + kB / kW - 1) / (kB / kW), (uint64_t)ctx->cu_count * 32);
+    if (A->n_rows && B->n_cols) {
+        // window: all columns when they fit kMaxWinBits, rounded to whole 64-word blocks
+        const uint64_t cols = std::min<uint64_t>(B->n_cols, kMaxWinBits);
+        const uint32_t win = (uint32_t)((cols + 2047) / 2048 * 2048);
+        const size_t lds = (size_t)kWpb * 2 * (win / 32) * 4;
+        const unsigned g = (unsigned)std::min<uint64_t>((A->n_rows + kWpb - 1) / kWpb, (uint64_t)ctx->cu_count * 8);
         if (A->dtype == SLAT_F64)
-            hipLaunchKernelGGL((k_dense_out<double, true>), dim3(g), dim3(kB), 0, s, A->row_ptr, A->col_idx,
+            hipLaunchKernelGGL((k_dense_out<double>), dim3(g), dim3(kB), lds, s, A->row_ptr, A->col_idx,
                                (const double *)A->values, B->row_ptr, B->col_idx, (const double *)B->values, A->n_rows,
-                               B->n_rows, (double *)dout, ld, transpose);
+                               B->n_rows, B->n_cols, win, (double *)dout, ld, transpose);
         else
-            hipLaunchKernelGGL((k_dense_out<uint32_t, false>), dim3(g), dim3(kB), 0, s, A->row_ptr, A->col_idx,
+            hipLaunchKernelGGL((k_dense_out<uint32_t>), dim3(g), dim3(kB), lds, s, A->row_ptr, A->col_idx,
                                (const uint32_t *)A->values, B->row_ptr, B->col_idx, (const uint32_t *)B->values,
-                               A->n_rows, B->n_rows, (uint32_t *)dout, ld, transpose);
+                               A->n_rows, B->n_rows, B->n_cols, win, (uint32_t *)dout, ld, transpose);
         if (hipGetLastError() != hipSuccess) {
             if (dout != out) slat_dev_free(ctx, dout, s);
             return fail(ctx, SLAT_EHIP, "dense output launch failed");

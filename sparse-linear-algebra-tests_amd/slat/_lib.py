@@ -21,6 +21,7 @@ EXPORTS = [
     "slat_last_error", "slat_get_stats", "slat_sync", "slat_csr_create", "slat_csr_to_host", "slat_csr_free",
     "slat_csr_view_of", "slat_csr_max_row_nnz", "slat_spgemm", "slat_spgemm_csr_u32", "slat_spgemm_csr_sat64",
     "slat_spgemm_csr_f64", "slat_spgemm_rowblock", "slat_rng_seed", "slat_rng_next_u64", "slat_rng_next_f64",
+    "slat_rng_next_u32", "slat_rng_range_u32", "slat_host_random",
     "slat_host_from_coo", "slat_host_lattice", "slat_host_thin", "slat_host_rmat", "slat_host_csr_free",
     "slat_csr_add", "slat_csr_identity", "slat_csr_pattern_equal", "slat_reachability_sum",
     "slat_power_until_stable", "slat_connected_components", "slat_csr_from_coo", "slat_csr_lattice", "slat_csr_thin",
@@ -107,6 +108,9 @@ def lib():
         "slat_rng_seed": ([P(RngState), C.c_char_p], None),
         "slat_rng_next_u64": ([P(RngState)], u64),
         "slat_rng_next_f64": ([P(RngState)], C.c_double),
+        "slat_rng_next_u32": ([P(RngState)], u32),
+        "slat_rng_range_u32": ([P(RngState), u32, u32], u32),
+        "slat_host_random": ([P(RngState), u32, u64, P(HostCsr)], C.c_int),
         "slat_host_from_coo": ([u64, u64, vp, vp, vp, i32, P(HostCsr)], C.c_int),
         "slat_host_lattice": ([P(u64), C.c_int, C.c_int, P(HostCsr)], C.c_int),
         "slat_host_thin": ([P(HostCsr), P(RngState), C.c_double, P(HostCsr)], C.c_int),

@@ -89,6 +89,13 @@ class StdRng:
     def random_f64(self) -> float:
         return float(L.lib().slat_rng_next_f64(C.byref(self._s)))
 
+    def next_u32(self) -> int:
+        return int(L.lib().slat_rng_next_u32(C.byref(self._s)))
+
+    def random_range(self, lo: int, hi: int) -> int:
+        """`rng.random_range(lo..hi)` for usize / u32 bounds (rand 0.9: u32 Canon's method)."""
+        return int(L.lib().slat_rng_range_u32(C.byref(self._s), lo, hi))
+
 
 # ------------------------------------------------------------------------------------------------
 # host CSR (numpy) produced by the library's constructors
@@ -159,6 +166,13 @@ def host_thin(m: HostCsr, rng: StdRng, density: float) -> HostCsr:
     raw = m._raw()
     h = L.HostCsr()
     L.check(L.lib().slat_host_thin(C.byref(raw), C.byref(rng._s), float(density), C.byref(h)))
+    return HostCsr._take(h)
+
+
+def host_random(rng: StdRng, n: int, m: int) -> HostCsr:
+    """CsrMatrix::random (src/graph_csr.rs:163-174) on the host: m edge draws, no self-loops."""
+    h = L.HostCsr()
+    L.check(L.lib().slat_host_random(C.byref(rng._s), n, m, C.byref(h)))
     return HostCsr._take(h)
 
 
@@ -239,6 +253,11 @@ class DeviceCsr:
         out = L.CsrOwned()
         L.check(L.lib().slat_csr_identity(ctx.ptr, n, cls.DTYPE, C.byref(out)), ctx.ptr)
         return cls(out, ctx)
+
+    @classmethod
+    def random(cls, rng: StdRng, n: int, m: int, ctx: Context | None = None):
+        """CsrMatrix::random (src/graph_csr.rs:163-174): the reference's draws, then to the device."""
+        return cls.from_host(host_random(rng, n, m), ctx)
 
     @classmethod
     def from_coo(cls, n: int, triplets: Iterable):

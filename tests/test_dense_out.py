@@ -79,6 +79,80 @@ def test_dense_out_matches_oracle(ctx, dtype, transpose, n, nnz):
                                   want.view(np.uint64) if dtype == O.F64 else want)
 
 
+def _relisted_pair(dtype):
+    """Operands whose running sums pass through 0 in the reference's visiting order (A row entries
+    ascending, then the B row): the column is listed twice in nz_cols and ends at 0
+    (einsum-dyn/src/sparse.rs:126-143)."""
+    if dtype == O.U32:
+        big, m1 = 65536, 0xFFFFFFFF
+        # (row 0, col 3): 65536*65536 wraps to 0, then +5  -> listed twice -> 0
+        # (row 1, col 3): 65536, then 65536*65536 (= +0)   -> listed once  -> 65536
+        # (row 2, col 0): 0xFFFFFFFF + 1 = 0, then +7      -> listed twice -> 0
+        # (row 3, col 0): 0xFFFFFFFF + 1 = 0 at the end     -> listed once  -> 0 (the sum)
+        ta = [(0, 1, big), (0, 2, 1), (1, 1, 1), (1, 4, big), (2, 5, m1), (2, 6, 1), (2, 7, 1), (3, 5, m1), (3, 6, 1)]
+        tb = [(1, 3, big), (2, 3, 5), (4, 3, big), (5, 0, 1), (6, 0, 1), (7, 0, 7), (1, 2, 5)]
+    else:
+        # row 0: 1.5 - 1.5 + 2 -> 0 ; row 1: 2 + 1.5 - 1.5 -> 2 ; row 2: 1e16 + 1 - 1e16 (not exact 0 midway)
+        ta = [(0, 1, 1.5), (0, 2, -1.5), (0, 4, 2.0), (1, 4, 2.0), (1, 5, 1.5), (1, 6, -1.5), (2, 7, 1e16), (2, 8, 1.0),
+              (2, 9, -1e16)]
+        tb = [(1, 3, 1.0), (2, 3, 1.0), (4, 3, 1.0), (5, 3, 1.0), (6, 3, 1.0), (7, 3, 1.0), (8, 3, 1.0), (9, 3, 1.0)]
+    n = 10
+    return coo(n, ta, dtype), coo(n, tb, dtype)
+
+
+def test_oracle_relisted_columns_end_at_zero():
+    for dtype in (O.U32, O.F64):
+        oa, ob = _relisted_pair(dtype)
+        vt = np.uint32 if dtype == O.U32 else np.float64
+        out = O.einsum_sparse_driven(oa, ob, np.full((10, 10), 9, vt))
+        if dtype == O.U32:
+            assert (out[0, 3], out[1, 3], out[2, 0], out[3, 0]) == (0, 65536, 0, 0)
+            assert out[1, 2] == 5 and out[0, 2] == 65536 * 5 and out[0, 0] == 9
+        else:
+            assert out[0, 3] == 0.0 and out[1, 3] == 2.0 and out[2, 3] == (1e16 + 1.0) - 1e16
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [O.U32, O.F64])
+@pytest.mark.parametrize("transpose", [False, True])
+def test_dense_out_relisted_columns(ctx, dtype, transpose):
+    # u32 65536*65536 wraps and f64 +x/-x cancellations: bit-exact with the oracle's listing semantics
+    oa, ob = _relisted_pair(dtype)
+    cls = slat.CsrMatrix if dtype == O.U32 else slat.CsrF64
+    da = cls.from_host(slat.HostCsr(10, *oa.arrays(), dtype), ctx)
+    db = cls.from_host(slat.HostCsr(10, *ob.arrays(), dtype), ctx)
+    vt = np.uint32 if dtype == O.U32 else np.float64
+    init = np.full((10, 12), 9, vt)
+    want = O.einsum_sparse_driven(oa, ob, init.copy(), transpose)
+    got = da.einsum_sparse_driven(db, init.copy(), transpose)
+    np.testing.assert_array_equal(got.view(np.uint64) if dtype == O.F64 else got,
+                                  want.view(np.uint64) if dtype == O.F64 else want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [O.U32, O.F64])
+@pytest.mark.parametrize("transpose", [False, True])
+def test_dense_out_frequent_cancellation(ctx, dtype, transpose):
+    # values +-1 (f64) / 1 and 0xFFFFFFFF (u32 wrap): running sums hit 0 all the time
+    g = np.random.default_rng(7 + dtype)
+    n, nnz = 400, 6000
+    if dtype == O.F64:
+        va, vb = g.choice([1.0, -1.0], nnz), g.choice([1.0, -1.0, 2.0], nnz)
+    else:
+        va, vb = g.choice([1, 0xFFFFFFFF, 65536], nnz), g.choice([1, 0xFFFFFFFF, 65536], nnz)
+    oa = O.from_coo(n, g.integers(0, n, nnz), g.integers(0, n, nnz), va, dtype)
+    ob = O.from_coo(n, g.integers(0, n, nnz), g.integers(0, n, nnz), vb, dtype)
+    cls = slat.CsrMatrix if dtype == O.U32 else slat.CsrF64
+    da = cls.from_host(slat.HostCsr(n, *oa.arrays(), dtype), ctx)
+    db = cls.from_host(slat.HostCsr(n, *ob.arrays(), dtype), ctx)
+    vt = np.uint32 if dtype == O.U32 else np.float64
+    init = np.full((n, n), 3, vt)
+    want = O.einsum_sparse_driven(oa, ob, init.copy(), transpose)
+    got = da.einsum_sparse_driven(db, init.copy(), transpose)
+    np.testing.assert_array_equal(got.view(np.uint64) if dtype == O.F64 else got,
+                                  want.view(np.uint64) if dtype == O.F64 else want)
+
+
 @pytest.mark.gpu
 def test_dense_out_torus_equals_saturating_product_when_no_overflow(ctx):
     # small counts: plain u32 = Saturating<u32>, so the dense output equals densify(A*A)

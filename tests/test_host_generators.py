@@ -53,3 +53,63 @@ def test_rmat_is_seeded_and_positive():
     b = slat.host_rmat(10, 8000)
     np.testing.assert_array_equal(a.col_idx, b.col_idx)
     assert a.values.min() >= 0.5 and a.n == 1024
+
+
+# CsrMatrix::random (src/graph_csr.rs:163-174). Pins: the reference's einsum study draws three 4/26
+# thins and then two random graphs from one StdRng seeded [42;32] (src/graph_csr.rs:1652-1669) and
+# prints their nnz (SPARSE_EINSUM_APPROACHES.md:127-132): 4070, 13844, 31936, then 4987 and 9983.
+# The integer draws follow rand 0.9's random_range for usize (UniformUsize -> u32, Canon's method);
+# rand 0.8's Lemire sampler would give 4988 / 9988 and a u64 Canon sampler 4992 / 9991.
+EINSUM_STUDY_NNZ = {"thin": [4070, 13844, 31936], "random": [4987, 9983]}
+
+
+def _einsum_study(mk_rng, thin, random):
+    rng = mk_rng()
+    thins = [thin(rng, s).nnz for s in (10, 15, 20)]
+    rands = [random(rng, n, m) for n, m in ((1000, 5000), (2000, 10000))]
+    return thins, rands
+
+
+def test_random_oracle_pinned_by_reference_nnz():
+    thins, rands = _einsum_study(O.Rng, lambda rng, s: O.thin(O.lattice([s, s, s], True), rng, 4.0 / 26.0),
+                                 lambda rng, n, m: O.random(rng, n, m))
+    assert thins == EINSUM_STUDY_NNZ["thin"]
+    assert [r.nnz for r in rands] == EINSUM_STUDY_NNZ["random"]
+
+
+def test_random_product_matches_oracle():
+    thins, rands = _einsum_study(slat.StdRng, lambda rng, s: slat.host_thin(slat.host_lattice([s, s, s], True), rng, 4.0 / 26.0),
+                                 lambda rng, n, m: slat.host_random(rng, n, m))
+    assert thins == EINSUM_STUDY_NNZ["thin"]
+    _, want = _einsum_study(O.Rng, lambda rng, s: O.thin(O.lattice([s, s, s], True), rng, 4.0 / 26.0),
+                            lambda rng, n, m: O.random(rng, n, m))
+    for got, w in zip(rands, want):
+        rp, col, val = w.arrays()
+        assert np.array_equal(got.row_ptr, rp) and np.array_equal(got.col_idx, col) and np.array_equal(got.values, val)
+        rows = np.repeat(np.arange(got.n), np.diff(got.row_ptr).astype(np.int64))
+        assert not np.any(rows == got.col_idx)  # no self-loops
+
+
+def test_rng_u32_and_straddling_u64_match_oracle():
+    # odd word positions: a u64 draw from the buffer's last word takes its high half from the refill
+    a, b = slat.StdRng(), O.Rng()
+    seq_a, seq_b = [], []
+    for i in range(700):
+        if i % 3 == 0:
+            seq_a.append(a.next_u32()), seq_b.append(b.next_u32())
+        elif i % 3 == 1:
+            seq_a.append(a.next_u64()), seq_b.append(b.next_u64())
+        else:
+            seq_a.append(a.random_range(0, 1000 + i)), seq_b.append(b.range_u32(0, 1000 + i))
+    assert seq_a == seq_b
+
+
+def test_rng_u64_straddle_word_order():
+    # BlockRng::next_u64 at index 63: (first word of the next refill) << 32 | buf[63]
+    r = O.Rng()
+    words = [r.next_u32() for _ in range(128)]
+    r2 = O.Rng()
+    for _ in range(63):
+        r2.next_u32()
+    assert r2.next_u64() == words[63] | (words[64] << 32)
+    assert r2.next_u32() == words[65]
