@@ -8,6 +8,7 @@
  *   CsrMatrix::matmul_par   src/graph_csr.rs:350-484         slat_spgemm_csr_u32 (same result)
  *   MagnusMatrix::matmul    src/graph_magnus.rs:224-232      slat_spgemm_csr_sat64
  *   MagnusMatrix::matmul_seq src/graph_magnus.rs:234-242     slat_spgemm_csr_sat64
+ *   MagnusMatrix (usize cols) src/graph_magnus.rs:11-14,224-242  slat_magnus_matmul
  *   linalg Csr<u32,f64>::matmul{,_par} linalg/src/csr.rs:308-466  slat_spgemm_csr_f64
  *   CsrMatrix::from_coo     src/graph_csr.rs:83-129          slat_csr_from_coo (device) / slat_host_from_coo
  *   CsrMatrix::lattice      src/graph_csr.rs:177-222         slat_csr_lattice (device) / slat_host_lattice
@@ -32,7 +33,8 @@
  *     slat_csr_free. Nothing is cached across calls except scratch in the context.
  *   * Layout = the reference's: row_ptr u64 (usize) [n_rows+1], col_idx u32 (NodeId) sorted and
  *     unique within a row, values u32 (saturating) | u64 (Sat64, saturating) | f64; no explicit
- *     zeros in outputs. MagnusMatrix's usize column indices are narrowed to u32 (n < 2^32).
+ *     zeros in outputs. slat_spgemm_csr_sat64 takes MagnusMatrix with u32 column ids;
+ *     slat_magnus_matmul takes its usize (u64) column ids as they are.
  *   * Results equal CsrMatrix::matmul bit for bit (u32 / Sat64; order-independent because values
  *     are non-negative) and the linalg f64 left fold in A-row order bit for bit (f64).
  *   * One slat_ctx per host thread / stream. Calls are synchronous on the context's stream.
@@ -143,6 +145,39 @@ slat_status slat_spgemm_csr_f64(slat_ctx *ctx, const slat_csr_view *A, const sla
  * row-block partition used across GPUs. */
 slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
                                  uint64_t row_end, const slat_csr_view *B, slat_csr *C, uint32_t flags);
+
+/* --- MagnusMatrix in its own layout (src/graph_magnus.rs:11-14) --------------------------------
+ * magnus::SparseMatrixCSR<Sat64>: row_ptr usize, col_idx usize (8-byte ids), values Sat64 (u64).
+ * slat_magnus_matmul replaces MagnusMatrix::matmul / matmul_seq (src/graph_magnus.rs:224-242)
+ * without narrowing or widening the Rust Vecs on the host: the columns are narrowed to u32 on the
+ * device (a column id >= n_cols -> SLAT_EINVAL; n_cols >= 2^32 -> SLAT_ENOTSUP), the Sat64 SpGEMM
+ * runs, and C's columns come back as u64. Release the result with slat_magnus_free. */
+typedef struct {
+    uint64_t n_rows, n_cols, nnz;
+    const uint64_t *row_ptr;
+    const uint64_t *col_idx;
+    const uint64_t *values;
+    int32_t residency; /* slat_residency */
+    int32_t _pad;
+    uint64_t max_row_nnz; /* 0 = unknown */
+} slat_magnus_view;
+
+typedef struct {
+    uint64_t n_rows, n_cols, nnz, capacity, max_row_nnz;
+    uint64_t *row_ptr;
+    uint64_t *col_idx;
+    uint64_t *values;
+    int32_t device;
+    int32_t _pad;
+    uint8_t _owner[96]; /* private: the blocks that hold the arrays */
+} slat_magnus;
+
+slat_status slat_magnus_matmul(slat_ctx *ctx, const slat_magnus_view *A, const slat_magnus_view *B,
+                               slat_magnus *C, uint32_t flags);
+slat_status slat_magnus_free(slat_ctx *ctx, slat_magnus *m);
+slat_status slat_magnus_to_host(slat_ctx *ctx, const slat_magnus *m, uint64_t *row_ptr, uint64_t *col_idx,
+                                uint64_t *values);
+slat_magnus_view slat_magnus_view_of(const slat_magnus *m);
 
 /* --- the reference's SpGEMM consumers, device-resident --------------
  * Square matrices (n_rows == n_cols) for the iterated drivers; host views are staged to the device.

@@ -1,11 +1,12 @@
 // slat_api.hip — C ABI (include/slat.h) over the gfx950 SpGEMM kernels.
 //
 // Orchestration of one C = A·B call on the context's stream:
-//   1. C.row_ptr and C.col/val in one device block of the context's cache (slat_dev_alloc). By
-//      default C is sized by the exact upper bound nnz(A)·max_row_nnz(B) (clamped to rows·cols),
-//      so no host round trip is needed between the symbolic and numeric passes; the capacity is
-//      recorded in slat_csr.capacity. SLAT_FLAG_EXACT_ALLOC (or a bound above 4 GiB / the budget)
-//      takes the reference's exact-size path instead: sync after the scan, allocate nnz(C).
+//   1. C.row_ptr, C.col and C.val in pieces of the context's device memory (slat_dev_alloc). By
+//      default col/val are sized by the exact upper bound nnz(A)·max_row_nnz(B) (clamped to
+//      rows·cols), so no host round trip is needed between the symbolic and numeric passes; at the
+//      end both are trimmed to nnz(C) and the tails return to the context's cache.
+//      SLAT_FLAG_EXACT_ALLOC (or a bound above 4 GiB / the budget) takes the reference's
+//      exact-size path instead: sync after the scan, allocate nnz(C).
 //   2. k_symbolic -> k_scan_rows (single-pass look-back scan) -> k_numeric, all stream-ordered.
 //   3. One D2H of the 64 status shards (nnz, max row nnz, dropped-zero rows) + stream sync.
 //   4. Rare: k_compact when explicit zeros were dropped.
@@ -25,6 +26,7 @@ using namespace slat;
 
 // max(B) for the CSR walk too (SLAT_NO_NARROW_CSR=1: the u64 slots of before, for A/B runs)
 static const bool kNarrowCsr = std::getenv("SLAT_NO_NARROW_CSR") == nullptr;
+static void dev_release_all(slat_ctx *ctx);
 
 extern "C" {
 
@@ -89,8 +91,7 @@ slat_status slat_ctx_destroy(slat_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
-    if (ctx->d_status) slat_dev_free(ctx, ctx->d_status, ctx->stream);
-    slat_dev_trim(ctx);
+    dev_release_all(ctx);
     if (ctx->h_shards) (void)hipHostFree(ctx->h_shards);
     if (ctx->d_words) (void)hipFree(ctx->d_words);
     if (ctx->h_out) (void)hipHostFree(ctx->h_out);
@@ -153,8 +154,10 @@ slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m) {
 }  // extern "C"
 
 // ---------------------------------------------------------------------------------------------
-// Device blocks (slat_internal.hpp). Sizes round to 4 KiB (to 2 MiB above 1 MiB) so repeated calls
-// of similar size find their block; a cached block serves a request of at least a quarter of it.
+// Device memory (slat_internal.hpp): hipMalloc'd chunks carved into pieces. Sizes round to 4 KiB (to
+// 2 MiB above 1 MiB) so repeated calls of similar size find their piece; a request takes the best-fit
+// free piece and splits off a remainder of 1 MiB or more; freed pieces merge with their free
+// neighbours; slat_dev_shrink hands the tail of a live piece back (C trimmed to nnz(C)).
 // Measured reason for not using hipMallocAsync (ROCm 7.2 image): after a thin call freed pool
 // blocks, a 324 MB lattice allocation read back zeros for a 26 MiB range of k_lattice's row writes
 // (the column writes of the same threads, in another range, were intact); with the default release
@@ -164,19 +167,52 @@ static size_t round_block(size_t b) {
     return (std::max<size_t>(b, 1) + g - 1) / g * g;
 }
 static constexpr size_t kCacheMax = (size_t)32 << 30;  // cached bytes kept at most (of 288 GB)
+static constexpr size_t kSplitMin = (size_t)1 << 20;   // smallest remainder kept as a piece of its own
+
+// a free piece into the cache, merged with the free neighbours of its chunk on the same stream
+static void cache_put(slat_ctx *ctx, slat_ctx::Block b) {
+    ctx->cache_bytes += b.bytes;
+    for (size_t i = 0; i < ctx->cache.size();) {
+        const auto &c = ctx->cache[i];
+        if (c.chunk == b.chunk && c.s == b.s &&
+            ((uint8_t *)c.p + c.bytes == (uint8_t *)b.p || (uint8_t *)b.p + b.bytes == (uint8_t *)c.p)) {
+            if (c.p < b.p) b.p = c.p;
+            b.bytes += c.bytes;
+            ctx->cache.erase(ctx->cache.begin() + (std::ptrdiff_t)i);
+            i = 0;  // the grown piece may now touch another
+            continue;
+        }
+        ++i;
+    }
+    ctx->cache.push_back(b);
+}
+
+static bool whole_chunk(const slat_ctx *ctx, const slat_ctx::Block &b) {
+    auto it = ctx->chunks.find(b.p);
+    return b.p == b.chunk && it != ctx->chunks.end() && it->second == b.bytes;
+}
 
 hipError_t slat_dev_alloc(slat_ctx *ctx, void **p, size_t bytes, hipStream_t s) {
     const size_t r = round_block(bytes);
+    // best fit on this stream: an exact-ish piece, or a larger one split (remainder >= kSplitMin)
     size_t best = SIZE_MAX;
     for (size_t i = 0; i < ctx->cache.size(); ++i) {
         const auto &c = ctx->cache[i];
-        if (c.s == s && c.bytes >= r && c.bytes / 4 <= r && (best == SIZE_MAX || c.bytes < ctx->cache[best].bytes)) best = i;
+        if (c.s != s || c.bytes < r) continue;
+        if (c.bytes / 4 > r && c.bytes - r < kSplitMin) continue;
+        if (best == SIZE_MAX || c.bytes < ctx->cache[best].bytes) best = i;
     }
     if (best != SIZE_MAX) {
-        *p = ctx->cache[best].p;
-        ctx->live[*p] = ctx->cache[best].bytes;
-        ctx->cache_bytes -= ctx->cache[best].bytes;
+        slat_ctx::Block c = ctx->cache[best];
         ctx->cache.erase(ctx->cache.begin() + (std::ptrdiff_t)best);
+        ctx->cache_bytes -= c.bytes;
+        if (c.bytes - r >= kSplitMin) {
+            ctx->cache_bytes += c.bytes - r;
+            ctx->cache.push_back({(uint8_t *)c.p + r, c.bytes - r, s, c.chunk});
+            c.bytes = r;
+        }
+        *p = c.p;
+        ctx->live[c.p] = c;
         return hipSuccess;
     }
     hipError_t e = hipMalloc(p, r);
@@ -185,32 +221,69 @@ hipError_t slat_dev_alloc(slat_ctx *ctx, void **p, size_t bytes, hipStream_t s) 
         slat_dev_trim(ctx);
         e = hipMalloc(p, r);
     }
-    if (e == hipSuccess) ctx->live[*p] = r;
+    if (e == hipSuccess) {
+        ctx->live[*p] = {*p, r, s, *p};
+        ctx->chunks[*p] = r;
+    }
     return e;
 }
 
 void slat_dev_free(slat_ctx *ctx, void *p, hipStream_t s) {
     auto it = ctx->live.find(p);
     if (it == ctx->live.end()) return;  // not ours (or freed already)
-    const size_t b = it->second;
+    slat_ctx::Block b = it->second;
     ctx->live.erase(it);
-    ctx->cache.push_back({p, b, s});
-    ctx->cache_bytes += b;
+    b.s = s;
+    cache_put(ctx, b);
     if (ctx->cache_bytes > kCacheMax) {
-        (void)hipDeviceSynchronize();  // the evicted blocks may still be read by queued work
-        while (ctx->cache_bytes > kCacheMax / 2 && !ctx->cache.empty()) {
-            ctx->cache_bytes -= ctx->cache.front().bytes;
-            (void)hipFree(ctx->cache.front().p);
-            ctx->cache.erase(ctx->cache.begin());
+        (void)hipDeviceSynchronize();  // the evicted chunks may still be read by queued work
+        for (size_t i = 0; i < ctx->cache.size() && ctx->cache_bytes > kCacheMax / 2;) {
+            if (whole_chunk(ctx, ctx->cache[i])) {
+                ctx->cache_bytes -= ctx->cache[i].bytes;
+                ctx->chunks.erase(ctx->cache[i].p);
+                (void)hipFree(ctx->cache[i].p);
+                ctx->cache.erase(ctx->cache.begin() + (std::ptrdiff_t)i);
+            } else {
+                ++i;
+            }
         }
     }
+}
+
+void slat_dev_shrink(slat_ctx *ctx, void *p, size_t bytes) {
+    auto it = ctx->live.find(p);
+    if (it == ctx->live.end()) return;
+    const size_t r = round_block(bytes);
+    slat_ctx::Block &b = it->second;
+    if (b.bytes < r + kSplitMin) return;  // not worth a piece
+    // the tail is free on the piece's stream from here on: work queued later on that stream runs
+    // after the work that wrote the kept head
+    cache_put(ctx, {(uint8_t *)p + r, b.bytes - r, b.s, b.chunk});
+    b.bytes = r;
 }
 
 void slat_dev_trim(slat_ctx *ctx) {
     if (ctx->cache.empty()) return;
     (void)hipDeviceSynchronize();
-    for (auto &c : ctx->cache) (void)hipFree(c.p);
+    for (size_t i = 0; i < ctx->cache.size();) {
+        if (whole_chunk(ctx, ctx->cache[i])) {
+            ctx->cache_bytes -= ctx->cache[i].bytes;
+            ctx->chunks.erase(ctx->cache[i].p);
+            (void)hipFree(ctx->cache[i].p);
+            ctx->cache.erase(ctx->cache.begin() + (std::ptrdiff_t)i);
+        } else {
+            ++i;  // part of a chunk that still holds live pieces
+        }
+    }
+}
+
+// context teardown: every chunk back to the driver, live pieces included
+static void dev_release_all(slat_ctx *ctx) {
+    (void)hipDeviceSynchronize();
+    for (auto &c : ctx->chunks) (void)hipFree(c.first);
+    ctx->chunks.clear();
     ctx->cache.clear();
+    ctx->live.clear();
     ctx->cache_bytes = 0;
 }
 
@@ -678,12 +751,17 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }();
     const unsigned __int128 budget = std::min<unsigned __int128>(ctx->free_b / 4, kBoundBytes);
     const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
+    // C's arrays in three pieces: row_ptr, then col_idx and values sized by the bound; after the
+    // call both are trimmed to nnz(C) and their tails go back to the context's cache
+    SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&C->row_ptr, (n + 1) * 8, s));
+    C->alloc = kAllocSeparate;
     if (!exact) {
         C->capacity = (uint64_t)std::max<unsigned __int128>(bound128, 1);
-        SLAT_HIP(ctx, alloc_joint(ctx, C, n, C->capacity, vs, s));
-    } else {
-        SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&C->row_ptr, (n + 1) * 8, s));
-        C->alloc = kAllocSeparate;
+        if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
+            slat_dev_alloc(ctx, &C->values, C->capacity * vs, s) != hipSuccess) {
+            slat_csr_free(ctx, C);
+            return fail(ctx, SLAT_EOOM, "C allocation failed");
+        }
     }
     a.c_rp = C->row_ptr;
 
@@ -868,6 +946,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     C->nnz = nnz;
     C->max_row_nnz = maxrow;
+    if (C->capacity > nnz) {
+        // trim the bound-sized arrays to nnz(C): the tails serve later allocations of the context
+        slat_dev_shrink(ctx, C->col_idx, std::max<uint64_t>(nnz, 1) * 4);
+        slat_dev_shrink(ctx, C->values, std::max<uint64_t>(nnz, 1) * vs);
+        C->capacity = std::max<uint64_t>(nnz, 1);
+    }
 
     slat_stats &S = ctx->stats;
     S.nnz = nnz;

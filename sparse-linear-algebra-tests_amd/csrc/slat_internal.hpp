@@ -34,15 +34,19 @@ struct slat_ctx {
     size_t free_b = 0;                       // cached hipMemGetInfo free bytes
     uint32_t free_age = 0;
     hipEvent_t ev[6] = {};
-    // device blocks: hipMalloc'd, cached after free and reused in stream order (slat_dev_alloc)
+    // device memory: hipMalloc'd chunks carved into pieces. A freed piece is cached and handed out
+    // again in stream order (slat_dev_alloc); adjacent free pieces of a chunk merge; a chunk goes
+    // back to the driver only when it is one free piece again.
     struct Block {
         void *p;
         size_t bytes;
         hipStream_t s;
+        void *chunk;  // the hipMalloc'd base this piece belongs to
     };
-    std::vector<Block> cache;                  // freed blocks, oldest first
+    std::vector<Block> cache;                  // free pieces, oldest first
     size_t cache_bytes = 0;
-    std::unordered_map<void *, size_t> live;   // allocated block -> its size
+    std::unordered_map<void *, Block> live;    // allocated piece -> its extent
+    std::unordered_map<void *, size_t> chunks; // hipMalloc'd base -> its size
     slat_stats stats = {};
 };
 
@@ -75,6 +79,8 @@ static inline size_t joint_bytes(uint64_t nrows, uint64_t cap, size_t vs) {
 // writes to part of a freshly grown block ("Device memory").
 hipError_t slat_dev_alloc(slat_ctx *ctx, void **p, size_t bytes, hipStream_t s);
 void slat_dev_free(slat_ctx *ctx, void *p, hipStream_t s);
+// keep the first `bytes` of live piece p and cache the rest (a bound-sized C trimmed to its nnz)
+void slat_dev_shrink(slat_ctx *ctx, void *p, size_t bytes);
 void slat_dev_trim(slat_ctx *ctx);  // device sync, then every cached block back to the driver
 
 // One block of the layout above.

@@ -27,6 +27,7 @@ EXPORTS = [
     "slat_power_until_stable", "slat_connected_components", "slat_csr_from_coo", "slat_csr_lattice", "slat_csr_thin",
     "slat_load_edges", "slat_edges_free", "slat_csr_from_edges", "slat_rcm_order", "slat_csr_permute",
     "slat_bandwidth_stats", "slat_spgemm_dense", "slat_device_alloc", "slat_device_free", "slat_device_copy",
+    "slat_magnus_matmul", "slat_magnus_free", "slat_magnus_to_host", "slat_magnus_view_of",
 ]
 
 
@@ -47,6 +48,18 @@ class CsrOwned(C.Structure):
                 ("max_row_nnz", C.c_uint64), ("row_ptr", C.c_void_p), ("col_idx", C.c_void_p),
                 ("values", C.c_void_p), ("dtype", C.c_int32), ("device", C.c_int32), ("alloc", C.c_int32),
                 ("_pad", C.c_int32)]
+
+
+class MagnusView(C.Structure):
+    _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_uint64), ("nnz", C.c_uint64), ("row_ptr", C.c_void_p),
+                ("col_idx", C.c_void_p), ("values", C.c_void_p), ("residency", C.c_int32), ("_pad", C.c_int32),
+                ("max_row_nnz", C.c_uint64)]
+
+
+class MagnusOwned(C.Structure):
+    _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_uint64), ("nnz", C.c_uint64), ("capacity", C.c_uint64),
+                ("max_row_nnz", C.c_uint64), ("row_ptr", C.c_void_p), ("col_idx", C.c_void_p),
+                ("values", C.c_void_p), ("device", C.c_int32), ("_pad", C.c_int32), ("_owner", C.c_uint8 * 96)]
 
 
 class Stats(C.Structure):
@@ -135,6 +148,10 @@ def lib():
         "slat_device_alloc": ([vp, u64, P(vp)], C.c_int),
         "slat_device_free": ([vp, vp], C.c_int),
         "slat_device_copy": ([vp, vp, vp, u64, i32], C.c_int),
+        "slat_magnus_matmul": ([vp, P(MagnusView), P(MagnusView), P(MagnusOwned), u32], C.c_int),
+        "slat_magnus_free": ([vp, P(MagnusOwned)], C.c_int),
+        "slat_magnus_to_host": ([vp, P(MagnusOwned), vp, vp, vp], C.c_int),
+        "slat_magnus_view_of": ([P(MagnusOwned)], MagnusView),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

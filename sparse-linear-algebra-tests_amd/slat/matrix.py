@@ -534,6 +534,64 @@ class MagnusMatrix(DeviceCsr):
         return self._spgemm(other)
 
 
+class MagnusMatrixUsize:
+    """`MagnusMatrix` in the reference's own layout (src/graph_magnus.rs:11-14): magnus's
+    SparseMatrixCSR<Sat64> with usize (u64) column ids, device-resident (slat_magnus)."""
+
+    def __init__(self, owned: L.MagnusOwned, ctx: Context):
+        self._m = owned
+        self._ctx = ctx
+
+    def __del__(self):
+        try:
+            if self._m is not None and self._m.row_ptr:
+                L.lib().slat_magnus_free(self._ctx.ptr, C.byref(self._m))
+        except Exception:
+            pass
+
+    @staticmethod
+    def host_view(n: int, row_ptr, col_idx, values, n_cols: int | None = None) -> L.MagnusView:
+        """A host view over u64 arrays (kept alive by the caller)."""
+        v = L.MagnusView()
+        v.n_rows, v.n_cols, v.nnz = n, n if n_cols is None else n_cols, len(col_idx)
+        v.row_ptr, v.col_idx, v.values = row_ptr.ctypes.data, col_idx.ctypes.data, values.ctypes.data
+        v.residency = L.HOST
+        return v
+
+    @staticmethod
+    def matmul_host(a: L.MagnusView, b: L.MagnusView, ctx: Context | None = None) -> "MagnusMatrixUsize":
+        ctx = ctx or default_context()
+        out = L.MagnusOwned()
+        L.check(L.lib().slat_magnus_matmul(ctx.ptr, C.byref(a), C.byref(b), C.byref(out), 0), ctx.ptr)
+        return MagnusMatrixUsize(out, ctx)
+
+    def view(self) -> L.MagnusView:
+        return L.lib().slat_magnus_view_of(C.byref(self._m))
+
+    def matmul(self, other: "MagnusMatrixUsize") -> "MagnusMatrixUsize":
+        """MagnusMatrix::matmul (src/graph_magnus.rs:225-232) with usize columns in and out."""
+        return MagnusMatrixUsize.matmul_host(self.view(), other.view(), self._ctx)
+
+    matmul_seq = matmul  # src/graph_magnus.rs:235-242: the same product
+
+    @property
+    def n(self) -> int:
+        return int(self._m.n_rows)
+
+    def nnz(self) -> int:
+        return int(self._m.nnz)
+
+    def host(self):
+        """(row_ptr u64, col_idx u64, values u64) host arrays."""
+        n, z = self.n, self.nnz()
+        rp = np.empty(n + 1, np.uint64)
+        col = np.empty(max(z, 1), np.uint64)
+        val = np.empty(max(z, 1), np.uint64)
+        L.check(L.lib().slat_magnus_to_host(self._ctx.ptr, C.byref(self._m), rp.ctypes.data, col.ctypes.data,
+                                            val.ctypes.data), self._ctx.ptr)
+        return rp, col[:z], val[:z]
+
+
 class Csr(DeviceCsr):
     """`linalg::csr::Csr<u32, V>` (linalg/src/csr.rs:93) with V chosen by `dtype`."""
 

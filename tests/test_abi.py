@@ -4,7 +4,6 @@ import os
 import re
 import subprocess
 
-import pytest
 
 import slat
 from slat import _lib as L
@@ -37,8 +36,7 @@ def test_library_loads_and_reports_no_device_here():
 
 
 def test_kernels_built_for_gfx950():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", L.LIB_PATH], capture_output=True,
-                         text=True, cwd="/tmp")
-    if out.returncode != 0:
-        pytest.skip("llvm-objdump --offloading unavailable")
-    assert "gfx950" in out.stdout + out.stderr or os.path.exists(L.LIB_PATH)
+    """The offload bundle inside libslat.so holds gfx950 code objects and no other GPU target."""
+    blob = open(L.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"hipv4-amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", blob))
+    assert targets == {b"gfx950"}, targets

@@ -1,0 +1,72 @@
+"""MagnusMatrix in the reference's own layout (src/graph_magnus.rs:11-14: usize column ids, Sat64
+values) through slat_magnus_matmul: u64 columns in and out, bit-exact against the oracle's Sat64
+CSR product (the MagnusMatrix results equal CsrMatrix's on Sat64, src/graph_magnus.rs:751-753)."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+import slat
+
+pytestmark = pytest.mark.gpu
+
+
+def _arrays(o: O.Csr):
+    rp, col, val = o.arrays()
+    return rp.astype(np.uint64), col.astype(np.uint64), val.astype(np.uint64)
+
+
+def _check(got: slat.MagnusMatrixUsize, want: O.Csr):
+    rp, col, val = got.host()
+    wrp, wcol, wval = want.arrays()
+    assert got.nnz() == want.nnz
+    assert col.dtype == np.uint64
+    np.testing.assert_array_equal(rp, wrp)
+    np.testing.assert_array_equal(col, wcol.astype(np.uint64))
+    np.testing.assert_array_equal(val, wval)
+
+
+@pytest.mark.parametrize("side,epn", [(10, 3.0), (30, 3.0)])
+def test_torus_chain_usize_cols(side, epn):
+    A = O.convert(O.torus_thinned(side, epn, O.Rng()), O.SAT64)
+    a = _arrays(A)
+    va = slat.MagnusMatrixUsize.host_view(A.n, *a)
+    P = slat.MagnusMatrixUsize.matmul_host(va, va)
+    want = O.matmul_seq(A, A)
+    _check(P, want)
+    for _ in range(2):  # A^3, A^4: device-resident left operand, host right operand
+        P = slat.MagnusMatrixUsize.matmul_host(P.view(), va, P._ctx)
+        want = O.matmul_seq(want, A)
+        _check(P, want)
+    assert P.matmul_seq(P).nnz() == P.matmul(P).nnz()
+
+
+def test_saturating_values_usize_cols():
+    rng = np.random.default_rng(7)
+    n, m = 300, 3000
+    r = rng.integers(0, n, m)
+    c = rng.integers(0, n, m)
+    v = rng.integers(1, 2**40, m, dtype=np.uint64)  # products overflow u64: Sat64 clamps
+    A = O.from_coo(n, r, c, v, O.SAT64)
+    a = _arrays(A)
+    va = slat.MagnusMatrixUsize.host_view(n, *a)
+    _check(slat.MagnusMatrixUsize.matmul_host(va, va), O.matmul_seq(A, A))
+
+
+def test_column_out_of_range_is_an_error():
+    rp = np.array([0, 1, 1], np.uint64)
+    col = np.array([2**32 + 1], np.uint64)  # a usize id no u32 can hold
+    val = np.array([1], np.uint64)
+    v = slat.MagnusMatrixUsize.host_view(2, rp, col, val)
+    with pytest.raises(slat.SlatError) as e:
+        slat.MagnusMatrixUsize.matmul_host(v, v)
+    assert e.value.status == 1  # SLAT_EINVAL (the reference would index out of bounds and panic)
+
+
+def test_dimension_mismatch_usize():
+    rp = np.zeros(3, np.uint64)
+    e = np.zeros(0, np.uint64)
+    a = slat.MagnusMatrixUsize.host_view(2, rp, e, e)
+    b = slat.MagnusMatrixUsize.host_view(3, np.zeros(4, np.uint64), e, e)
+    with pytest.raises(slat.SlatError) as ex:
+        slat.MagnusMatrixUsize.matmul_host(a, b)
+    assert ex.value.status == 2
