@@ -203,7 +203,7 @@ def main():
                     "kernel": "k_numeric", "algorithmic_bytes": alg, "timed_steps": len(num),
                     "kernel_ms": {"symbolic": round(float(np.mean(sym)), 4), "scan": round(float(np.mean(scan)), 4),
                                   "numeric": round(num_ms, 4), "device_total": round(float(np.mean(tot)), 4)},
-                    "pipeline_frac": round(alg / (float(np.mean(tot)) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+                    "pipeline_frac": round(alg / (max(float(np.mean(tot)), 1e-6) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
         cpu = None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(side, power, args.cpu_seconds)

@@ -1,8 +1,11 @@
 #!/bin/bash
-# usage: tools/build_variant.sh NAME "-DFLAG=..." — builds tools/bin/libslat_NAME.so (kernel experiments)
+# usage: tools/build_variant.sh NAME SRC "-DFLAG=..." — builds tools/bin/libslat_NAME.so with SRC
+# (e.g. slat_fused) compiled with the extra flags and the tree's other objects (kernel experiments)
 set -e
 mkdir -p "$(dirname "$0")/bin"
 cd "$(dirname "$0")/../sparse-linear-algebra-tests_amd"
 make -s
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I../include -Icsrc $2 -c csrc/slat_api.hip -o /tmp/slat_$1.o
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../tools/bin/libslat_$1.so /tmp/slat_$1.o build/slat_graph.o build/slat_coo.o build/slat_dense.o build/host_gen.o
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I../include -Icsrc $3 -c csrc/$2.hip -o /tmp/slat_$1.o
+objs=""
+for o in build/*.o; do [ "$o" = "build/$2.o" ] || objs="$objs $o"; done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../tools/bin/libslat_$1.so /tmp/slat_$1.o $objs
