@@ -27,10 +27,6 @@ using namespace slat;
 // max(B) for the CSR walk too (SLAT_NO_NARROW_CSR=1: the u64 slots of before, for A/B runs)
 static const bool kNarrowCsr = std::getenv("SLAT_NO_NARROW_CSR") == nullptr;
 static void dev_release_all(slat_ctx *ctx);
-static constexpr uint32_t kFlagNoFused = 0x80000000u;  // internal: the rerun after a fused launch gave up
-// slat_fused.hip: the one-kernel path (single-window launches with the ELL copy of B)
-slat_status slat_launch_fused(slat_ctx *ctx, const slat::Args &a, int32_t dtype, bool idx32, size_t lds);
-slat_status slat_fused_reset(slat_ctx *ctx);
 
 extern "C" {
 
@@ -76,7 +72,7 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         delete ctx;
         return SLAT_EOOM;
     }
-    if (hipMalloc((void **)&ctx->d_words, 128) != hipSuccess || hipMemset(ctx->d_words, 0, 128) != hipSuccess ||
+    if (hipMalloc((void **)&ctx->d_words, 64) != hipSuccess || hipMemset(ctx->d_words, 0, 64) != hipSuccess ||
         hipHostMalloc((void **)&ctx->h_out, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&ctx->h_out_dev, ctx->h_out, 0) != hipSuccess) {
         (void)hipHostFree(ctx->h_shards);
@@ -705,26 +701,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         size_t total_b = 0;
         (void)hipMemGetInfo(&ctx->free_b, &total_b);
     }
-    // capacity by exact bound (no mid-call sync) unless it exceeds the budget
-    unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
-    const unsigned __int128 dense = (unsigned __int128)n * ncols;
-    if (bound128 > dense) bound128 = dense;
-    // free device memory: refreshed every 32 calls above (the query costs host time on every call)
-    // and at most kBoundBytes: a loose bound (power-law B: nnz(A) x a hub row) would make every call
-    // allocate and release tens of GB, which costs far more than the exact path's one sync
-    static const uint64_t kBoundBytes = [] {
-        const char *e = std::getenv("SLAT_BOUND_MAX_BYTES");
-        return e ? std::strtoull(e, nullptr, 10) : (4ull << 30);
-    }();
-    const unsigned __int128 budget = std::min<unsigned __int128>(ctx->free_b / 4, kBoundBytes);
-    const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
-    // one kernel for symbolic, offsets and numeric (slat_fused.hip): one window covers every column,
-    // B has the ELL copy, integer values
-    static const bool kNoFused = std::getenv("SLAT_NO_FUSED") != nullptr;
-    const bool fused = !a.wide && ell && (dt == SLAT_U32 || dt == SLAT_SAT64) && !a.stats && !ablate && !exact &&
-                       !SLAT_PHASES && !kNoFused && !(flags & kFlagNoFused);
     const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
-    const bool sbm = !a.wide && !fused && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) &&
+    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) &&
                      !std::getenv("SLAT_NO_SBM");
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
@@ -758,8 +736,21 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         a.nblk = a.ww / kWave;
     }
     a.host_out = ctx->h_out_dev;
-    ctx->h_out[0] = ctx->h_out[1] = ctx->h_out[2] = ctx->h_out[3] = 0;  // no kernel of this context is in flight
+    ctx->h_out[0] = ctx->h_out[1] = ctx->h_out[2] = 0;  // no kernel of this context is in flight
 
+    // capacity by exact bound (no mid-call sync) unless it exceeds the budget
+    unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
+    const unsigned __int128 dense = (unsigned __int128)n * ncols;
+    if (bound128 > dense) bound128 = dense;
+    // free device memory: refreshed every 32 calls above (the query costs host time on every call)
+    // and at most kBoundBytes: a loose bound (power-law B: nnz(A) x a hub row) would make every call
+    // allocate and release tens of GB, which costs far more than the exact path's one sync
+    static const uint64_t kBoundBytes = [] {
+        const char *e = std::getenv("SLAT_BOUND_MAX_BYTES");
+        return e ? std::strtoull(e, nullptr, 10) : (4ull << 30);
+    }();
+    const unsigned __int128 budget = std::min<unsigned __int128>(ctx->free_b / 4, kBoundBytes);
+    const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
     // C's arrays in three pieces: row_ptr, then col_idx and values sized by the bound; after the
     // call both are trimmed to nnz(C) and their tails go back to the context's cache
     SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&C->row_ptr, (n + 1) * 8, s));
@@ -801,27 +792,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                            a.epoch);
         SLAT_HIP(ctx, hipGetLastError());
     }
-    if (fused) {
-        a.c_col = C->col_idx;
-        a.c_val = C->values;
-        if (timing) {
-            SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
-            SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
-            SLAT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
-        }
-        if ((st = slat_launch_fused(ctx, a, dt, idx32, num_lds))) {
-            slat_csr_free(ctx, C);
-            return st;
-        }
-        if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
-        SLAT_HIP(ctx, wait_stream(s));
-        if (ctx->h_out[3]) {
-            // the fused kernel gave up (its grid was not all resident): rerun on the three-kernel path
-            if ((st = slat_fused_reset(ctx))) return st;
-            slat_csr_free(ctx, C);
-            return slat_spgemm_rowblock(ctx, A, row_begin, row_end, B, C, flags | kFlagNoFused);
-        }
-    } else {
     if (ablate & 7u) {
         // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded
         Args abl = asym;
@@ -919,7 +889,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (a.stats) SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                              hipMemcpyDeviceToHost, s));
     SLAT_HIP(ctx, wait_stream(s));
-    }  // !fused
     if (SLAT_PHASES) {
         // diagnostic build: per-phase cycles of the numeric kernel, summed over waves
         unsigned long long ph[kPhaseSlots * 64];
@@ -952,7 +921,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&ncol, std::max<uint64_t>(total, 1) * 4, s));
         SLAT_HIP(ctx, slat_dev_alloc(ctx, &nval, std::max<uint64_t>(total, 1) * vs, s));
         if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
-        hipError_t e;
         if (dt == SLAT_U32)
             e = launch_compact<SemU32>(sym_grid, s, C->row_ptr, nrp, n, C->col_idx, C->values, ncol, nval);
         else if (dt == SLAT_SAT64)

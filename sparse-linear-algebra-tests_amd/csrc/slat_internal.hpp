@@ -22,23 +22,15 @@ struct slat_ctx {
     void *ws = nullptr;
     size_t ws_bytes = 0;
     unsigned long long *h_shards = nullptr;  // pinned (stats / max-row read-backs)
-    unsigned long long *h_out = nullptr;     // mapped pinned: [0] nnz, [1] max row nnz, [2] rows with zeros,
-                                             // [3] the fused kernel gave up
+    unsigned long long *h_out = nullptr;     // mapped pinned: [0] nnz, [1] max row nnz, [2] rows with zeros
     unsigned long long *h_out_dev = nullptr; // its device alias (written by k_scan_rows / k_numeric)
-    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word,
-                                             // [4] usize-column error word, [5] fused max-row word,
-                                             // [6] fused finished waves, [7] fused abort word (16 words)
+    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
     unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
     uint64_t status_cap = 0;                 // tiles d_status holds
     unsigned long long ticket_base = 0;      // tiles handed out so far (the ticket is monotonic)
     uint32_t scan_epoch = 0;                 // tag of the status / max-row words (22 bits)
-    // the fused kernel's look-back words (slat_fused.hip): rows | groups (epoch-tagged) | group counters
-    unsigned long long *lb_status = nullptr;
-    uint64_t lb_cap = 0;
-    uint32_t lb_epoch = 0;
-    unsigned long long lb_done = 0;
     size_t free_b = 0;                       // cached hipMemGetInfo free bytes
     uint32_t free_age = 0;
     hipEvent_t ev[6] = {};

@@ -1,5 +1,5 @@
 #!/bin/bash
-# bench A/B across library builds: ms/step and the per-kernel split
+# bench A/B across library builds (tree | nofused | a tools/bin/libslat_NAME.so variant): ms/step, kernel split
 set -o pipefail
 OUT=gpurun_out/${1:-fab}; shift
 mkdir -p $OUT
