@@ -8,10 +8,15 @@ saturating values, nnz(C) = 11,736,555. Inputs are device-resident before the ti
 step is one complete synchronous SpGEMM call (symbolic, scan, C allocation, numeric, nnz read-back)
 and its output is released inside the step.
 
-N > 1 (torchrun, one rank per GPU): `--scaling weak` (default) — the global matrix is the
-block-diagonal of N independent tori and rank r owns block r (1-D row partition, no data-path
-collective); `--scaling strong` — config C4, 100^3 torus A^3·A, rows split across ranks into
-flops-balanced blocks, B replicated. value = output nnz of all ranks / max-over-ranks time.
+N > 1 (torchrun, one rank per GPU): `--scaling strong` (default) — config C4, the 100^3 torus,
+C = A^3·A, whose rows are split across the ranks into flops-balanced blocks cut on the device
+(north_star: >= 6x strong scaling at 8 GPUs). Rank 0 builds A and A^3 and broadcasts them over
+RCCL (libslat's slat_bcast_csr, outside the timed region); each rank then times its row block with
+no data-path collective (C stays row-distributed, the next power's left operand). Rank 0 also times
+the whole product alone on its GPU afterwards and reports the speedup. `--gather` adds the
+allgatherv of C's row blocks over RCCL (slat_allgather_rows), timed separately as gather_ms.
+`--scaling weak` is the labelled extra: one 30^3 torus per rank (the block-diagonal matrix).
+value = output nnz of all ranks / max-over-ranks time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -88,7 +93,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=50, help="untimed steps; the GPU needs ~10 ms of load to clock up")
     ap.add_argument("--side", type=int, default=30)
     ap.add_argument("--power", type=int, default=7, help="C = A^(power-1) * A")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="N > 1 default: strong (config C4 split over the ranks); weak = one torus per rank")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--timing-every", type=int, default=4,
@@ -107,7 +113,8 @@ def main():
     # visible GPU(s) (the metric's runs use RCCL, "nccl")
     backend = os.environ.get("SLAT_DIST_BACKEND", "nccl")
     dev_index = local
-    if world > 1:
+    # SLAT_FORCE_DIST=1: the multi-rank code path even at world size 1 (one-GPU rehearsal)
+    if world > 1 or os.environ.get("SLAT_FORCE_DIST"):
         import torch
         import torch.distributed as dist
         if backend == "nccl":
@@ -119,16 +126,25 @@ def main():
     coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
 
     ctx = slat.Context(dev_index)
+    scaling = args.scaling or ("strong" if dist is not None else "weak")
     side, power = args.side, args.power
-    if args.scaling == "strong" and world > 1 and side == 30:
-        side, power = 100, 4
-    A, P = build_inputs(side, power, ctx)
+    if scaling == "strong" and dist is not None and side == 30 and power == 7:
+        side, power = 100, 4  # config C4: 100^3 torus, C = A^3 * A split over the ranks
+    comm = None
+    if dist is not None and scaling == "strong" and backend == "nccl":
+        # rank 0 builds the operands; B (= A) and the left operand reach the others over RCCL
+        # (one broadcast per array, outside the timed region)
+        comm = slat_dist.Comm(ctx)
+        A, P = build_inputs(side, power, ctx) if rank == 0 else (None, None)
+        A = comm.bcast(A, slat.CsrMatrix)
+        P = comm.bcast(P, slat.CsrMatrix)
+    else:
+        A, P = build_inputs(side, power, ctx)
     n = A.n
     row_lo, row_hi = 0, n
-    if args.scaling == "strong" and world > 1:
-        # flops-balanced 1-D row blocks of the left operand, B replicated
-        h, a = P.host(), A.host()
-        cuts = slat_dist.flops_balanced_cuts(h.row_ptr, h.col_idx, a.row_ptr, world)
+    if scaling == "strong" and dist is not None:
+        # flops-balanced 1-D row blocks of the left operand, cut on the device
+        cuts = slat_dist.device_cuts(P, A, world)
         row_lo, row_hi = cuts[rank], cuts[rank + 1]
 
     def step(flags=0):
@@ -176,19 +192,46 @@ def main():
     value = units / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
 
-    gather_ms = None
+    single_ms = None
+    if dist is not None and scaling == "strong":
+        # the same product on one GPU (rank 0 alone), for the strong-scaling speedup
+        dist.barrier()
+        if rank == 0:
+            k = max(5, min(args.steps, 20))
+            for _ in range(3):
+                P.matmul_rowblock(0, n, A, 0)
+            ctx.sync()
+            ts = time.perf_counter()
+            for _ in range(k):
+                C1 = P.matmul_rowblock(0, n, A, 0)
+                del C1
+            ctx.sync()
+            single_ms = (time.perf_counter() - ts) / k * 1e3
+        dist.barrier()
+
+    gather_ms, gather_nnz = None, None
     if dist is not None and args.gather:
         # not part of the SpGEMM metric: C row blocks stay distributed for the next step (§8(e))
         import torch
         C = P.matmul_rowblock(row_lo, row_hi, A, 0)
-        hc = C.host()
-        dist.barrier()
-        tg = time.perf_counter()
-        slat_dist.gather_blocks(hc.row_ptr, hc.col_idx, hc.values, device=torch.device(coll_dev))
-        if backend == "nccl":
-            torch.cuda.synchronize()
-        dist.barrier()
-        gather_ms = (time.perf_counter() - tg) * 1e3
+        if comm is not None:
+            # device-resident allgatherv over RCCL (libslat): u32 columns, native-width values
+            comm.allgather_rows(C)  # warm-up (RCCL connection setup)
+            dist.barrier()
+            tg = time.perf_counter()
+            full = comm.allgather_rows(C)
+            dist.barrier()
+            gather_ms = (time.perf_counter() - tg) * 1e3
+            gather_nnz = full.nnz()
+            del full
+        else:  # CPU rehearsal (gloo): the host restatement of the assembly
+            hc = C.host()
+            dist.barrier()
+            tg = time.perf_counter()
+            slat_dist.gather_blocks(hc.row_ptr, hc.col_idx, hc.values, device=torch.device(coll_dev))
+            dist.barrier()
+            gather_ms = (time.perf_counter() - tg) * 1e3
+            gather_nnz = None
         del C
 
     if rank == 0:
@@ -212,18 +255,23 @@ def main():
             "metric": "GNNZ/s (output nnz/s) for A×A on 30³ Moore torus, 1/2/4/8 GPUs",
             "value": round(value, 4), "unit": "GNNZ/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak" if args.scaling == "weak" else "strong",
+            "scaling": scaling,
             "vs_baseline": round(value / README_CSR_PAR_A7_GNNZ, 2) if (side, power) == (30, 7) else None,
             "dtype": "u32", "data": "synthetic (reference generator: ChaCha12 StdRng seed [42;32])",
             "config": {"workload": workload, "nnz_c": nnz_c, "n": n, "rows": [row_lo, row_hi],
-                       "partition": "block-diagonal, one torus per rank" if args.scaling == "weak" else "flops-balanced row blocks",
+                       "partition": "block-diagonal, one torus per rank" if scaling == "weak" else "flops-balanced row blocks",
                        "capacity": stats["capacity"], "mode": stats["mode"], "window_words": stats["window_words"],
                        **({"ablated_ms": round(float(np.mean(abl)), 4)} if os.environ.get("SLAT_ABLATE") else {}),
-                       **({"gather_ms": round(gather_ms, 3)} if gather_ms is not None else {})},
+                       **({"gather_ms": round(gather_ms, 3)} if gather_ms is not None else {}),
+                       **({"gather_nnz": gather_nnz} if gather_nnz is not None else {}),
+                       **({"single_gpu_ms": round(single_ms, 4), "strong_speedup": round(single_ms / ms_per_step, 3)}
+                          if single_ms is not None else {})},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

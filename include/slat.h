@@ -179,6 +179,26 @@ slat_status slat_magnus_to_host(slat_ctx *ctx, const slat_magnus *m, uint64_t *r
                                 uint64_t *values);
 slat_magnus_view slat_magnus_view_of(const slat_magnus *m);
 
+/* --- multi-GPU row blocks over RCCL -------------------------------------------
+ * One process per GPU. The reference splits matmul_par's output rows over rayon threads
+ * (src/graph_csr.rs:350-484); here rank r computes C rows [cuts[r], cuts[r+1]) with
+ * slat_spgemm_rowblock, B replicated. All calls are collective over the communicator (every rank
+ * calls them, in the same order) and run on the context's stream. */
+typedef struct slat_comm slat_comm;
+/* ncclGetUniqueId into id[128], on one rank; share it with the others out of band. */
+slat_status slat_comm_id(uint8_t id[128]);
+slat_status slat_comm_create(slat_ctx *ctx, int nranks, int rank, const uint8_t id[128], slat_comm **out);
+slat_status slat_comm_destroy(slat_comm *comm);
+/* Flops-balanced 1-D row cuts of A*B on the device (not collective): cuts[0..parts] (host array),
+ * cuts[r] = the first row whose running product count reaches r/parts of the total. */
+slat_status slat_rowblock_cuts(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, uint32_t parts,
+                               uint64_t *cuts);
+/* The root's matrix on every rank (non-roots: *m is overwritten with a new library-owned matrix). */
+slat_status slat_bcast_csr(slat_ctx *ctx, slat_comm *comm, slat_csr *m, int root);
+/* Allgatherv of the ranks' C row blocks, in rank order, into a new library-owned matrix `full` on every
+ * rank: row_ptr rebased on the device; payload nnz * (4 + value bytes) + rows * 8. */
+slat_status slat_allgather_rows(slat_ctx *ctx, slat_comm *comm, const slat_csr_view *block, slat_csr *full);
+
 /* --- the reference's SpGEMM consumers, device-resident --------------
  * Square matrices (n_rows == n_cols) for the iterated drivers; host views are staged to the device.
  * Loop decisions (nnz, pattern equality) are the only host round trips. */

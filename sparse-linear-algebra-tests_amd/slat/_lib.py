@@ -28,6 +28,8 @@ EXPORTS = [
     "slat_load_edges", "slat_edges_free", "slat_csr_from_edges", "slat_rcm_order", "slat_csr_permute",
     "slat_bandwidth_stats", "slat_spgemm_dense", "slat_device_alloc", "slat_device_free", "slat_device_copy",
     "slat_magnus_matmul", "slat_magnus_free", "slat_magnus_to_host", "slat_magnus_view_of",
+    "slat_comm_id", "slat_comm_create", "slat_comm_destroy", "slat_rowblock_cuts", "slat_bcast_csr",
+    "slat_allgather_rows",
 ]
 
 
@@ -152,6 +154,12 @@ def lib():
         "slat_magnus_free": ([vp, P(MagnusOwned)], C.c_int),
         "slat_magnus_to_host": ([vp, P(MagnusOwned), vp, vp, vp], C.c_int),
         "slat_magnus_view_of": ([P(MagnusOwned)], MagnusView),
+        "slat_comm_id": ([vp], C.c_int),
+        "slat_comm_create": ([vp, C.c_int, C.c_int, vp, P(vp)], C.c_int),
+        "slat_comm_destroy": ([vp], C.c_int),
+        "slat_rowblock_cuts": ([vp, P(CsrView), P(CsrView), u32, vp], C.c_int),
+        "slat_bcast_csr": ([vp, vp, P(CsrOwned), C.c_int], C.c_int),
+        "slat_allgather_rows": ([vp, vp, P(CsrView), P(CsrOwned)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -6,9 +6,12 @@ replicated (`slat_spgemm_rowblock`). Cuts are balanced by scalar products (flops
 so skewed (power-law) inputs split evenly. The reference has no multi-process path; its `matmul_par`
 (src/graph_csr.rs:350-484) splits rows across rayon threads the same way, dynamically.
 
-`gather_blocks` is the optional assembly of the distributed row blocks into one CSR on every rank
-(an allgatherv built from all_gather on padded tensors: RCCL/gloo have no native allgatherv). It is
-not part of the timed SpGEMM; bench.py reports it separately.
+On the GPUs everything runs through libslat's C ABI over RCCL (`Comm`): the cuts on the device
+(`slat_rowblock_cuts`), the replicated operand from rank 0 (`slat_bcast_csr`), and the optional
+assembly of the distributed row blocks into one CSR on every rank (`slat_allgather_rows`: one
+ncclBroadcast per root and array, u32 columns and native-width values, row_ptr rebased on the device).
+The host functions below restate the cut rule and the assembly in numpy for the CPU (gloo) rehearsal
+of the multi-rank flow and its tests; `gather_blocks` is that rehearsal's allgatherv.
 """
 from __future__ import annotations
 
@@ -25,19 +28,80 @@ def row_flops(a_rp: np.ndarray, a_col: np.ndarray, b_rp: np.ndarray) -> np.ndarr
 
 
 def flops_balanced_cuts(a_rp: np.ndarray, a_col: np.ndarray, b_rp: np.ndarray, parts: int) -> list[int]:
-    """Row boundaries [0, c1, ..., n] giving each of `parts` blocks about 1/parts of the products."""
+    """Row boundaries [0, c1, ..., n] giving each of `parts` blocks about 1/parts of the products
+    (no products at all: equal row counts). The rule slat_rowblock_cuts applies on the device."""
     if parts < 1:
         raise ValueError("parts must be >= 1")
     n = len(a_rp) - 1
     f = row_flops(a_rp, a_col, b_rp)
-    cum = np.cumsum(f)
-    total = int(cum[-1]) if n else 0
+    cum = np.cumsum(f).astype(object) * parts  # exact: cut r = first row with cum * parts >= total * r
+    total = int(cum[-1]) // parts if n else 0
     cuts = [0]
     for r in range(1, parts):
-        c = int(np.searchsorted(cum, total * r / parts, side="left")) if total else (n * r) // parts
+        c = int(np.searchsorted(cum, total * r, side="left")) if total else (n * r) // parts
         cuts.append(min(max(c, cuts[-1]), n))
     cuts.append(n)
     return cuts
+
+
+class Comm:
+    """An RCCL communicator of libslat (slat_comm): one rank per GPU, the unique id shared over the
+    torch.distributed group that launched the ranks."""
+
+    def __init__(self, ctx, group=None):
+        import ctypes as C
+
+        import torch.distributed as dist
+
+        from . import _lib as L
+        self._ctx = ctx
+        self.rank, self.size = dist.get_rank(group), dist.get_world_size(group)
+        uid = (C.c_uint8 * 128)()
+        if self.rank == 0:
+            L.check(L.lib().slat_comm_id(uid))
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0, group=group)
+        uid = (C.c_uint8 * 128).from_buffer_copy(box[0])
+        self._p = C.c_void_p()
+        L.check(L.lib().slat_comm_create(ctx.ptr, self.size, self.rank, uid, C.byref(self._p)), ctx.ptr)
+
+    def close(self):
+        from . import _lib as L
+        if self._p:
+            L.lib().slat_comm_destroy(self._p)
+            self._p = None
+
+    def bcast(self, m, cls, root: int = 0):
+        """The root's device matrix on every rank (others pass None)."""
+        import ctypes as C
+
+        from . import _lib as L
+        out = m._m if m is not None else L.CsrOwned()
+        L.check(L.lib().slat_bcast_csr(self._ctx.ptr, self._p, C.byref(out), root), self._ctx.ptr)
+        if m is not None:
+            return m
+        return cls(out, self._ctx)
+
+    def allgather_rows(self, block):
+        """C's row blocks of all ranks, in rank order, as one device matrix on every rank."""
+        import ctypes as C
+
+        from . import _lib as L
+        v = block.view()
+        out = L.CsrOwned()
+        L.check(L.lib().slat_allgather_rows(self._ctx.ptr, self._p, C.byref(v), C.byref(out)), self._ctx.ptr)
+        return type(block)(out, self._ctx)
+
+
+def device_cuts(A, B, parts: int) -> list[int]:
+    """flops_balanced_cuts computed on the device (slat_rowblock_cuts)."""
+    import ctypes as C
+
+    from . import _lib as L
+    cuts = (C.c_uint64 * (parts + 1))()
+    a, b = A.view(), B.view()
+    L.check(L.lib().slat_rowblock_cuts(A._ctx.ptr, C.byref(a), C.byref(b), parts, cuts), A._ctx.ptr)
+    return [int(c) for c in cuts]
 
 
 def _to_i64(a: np.ndarray) -> np.ndarray:
