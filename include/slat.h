@@ -19,6 +19,7 @@
  *   CsrMatrix::reachability_sum    src/graph_csr.rs:545-559  slat_reachability_sum
  *   CsrMatrix::power_until_stable  src/graph_csr.rs:562-577  slat_power_until_stable
  *   CsrMatrix::connected_components src/graph_csr.rs:580-603 slat_connected_components
+ *   bench_diameter (driver) src/graph_csr.rs:1228-1319       slat_diameter
  *   CsrMatrix::from_edges{,_undirected} src/graph_csr.rs:132-147 slat_csr_from_edges
  *   CsrMatrix::rcm          src/graph_csr.rs:663-722         slat_rcm_order + slat_csr_permute
  *   CsrMatrix::permute / unpermute src/graph_csr.rs:726-799  slat_csr_permute
@@ -70,6 +71,9 @@ typedef enum { SLAT_DEVICE = 0, SLAT_HOST = 1 } slat_residency;
  * reference's left fold in A-row order; results then agree with the reference within the stated
  * tolerance (relative 1e-12 for same-sign values), not bit for bit (config C5). */
 #define SLAT_FLAG_F64_ANY_ORDER 0x8u
+/* the 64-bit-offset kernel instances even when every offset fits 32 bits (they run by themselves
+ * once nnz(A) or nnz(B) reaches 2^32; the flag lets small inputs test them) */
+#define SLAT_FLAG_IDX64 0x10u
 
 typedef struct slat_ctx slat_ctx;
 
@@ -221,6 +225,13 @@ slat_status slat_power_until_stable(slat_ctx *ctx, const slat_csr_view *A, slat_
 /* CsrMatrix::connected_components (src/graph_csr.rs:580-603): closure of A + I, then component ids
  * numbered by smallest member; `component` = host array of n_rows u64 (usize). */
 slat_status slat_connected_components(slat_ctx *ctx, const slat_csr_view *A, uint64_t *component);
+
+/* bench_diameter's algorithm (src/graph_csr.rs:1228-1319) on the device: A = the undirected graph
+ * (from_edges_undirected); R0 = A + I squared until its pattern is stable, then the last power
+ * before stabilisation times R0 until stable. *diameter = the largest finite distance (1 when R0 is
+ * already its own closure); *squarings / *refinements = the products of each phase (may be NULL). */
+slat_status slat_diameter(slat_ctx *ctx, const slat_csr_view *A, uint64_t *diameter, uint64_t *squarings,
+                          uint64_t *refinements);
 
 /* --- host-side input generators (the reference's constructors) ------------------------------ */
 /* Host CSR owned by the library (malloc); free with slat_host_csr_free. */

@@ -237,6 +237,34 @@ def connected_components(a: Csr) -> np.ndarray:
     return out[:a.n]
 
 
+def diameter(a: Csr):
+    """bench_diameter (src/graph_csr.rs:1228-1319) over the oracle's matmul/add/identity: R0 = A + I;
+    repeated squaring until the pattern is stable, then the last power before it times R0 until
+    stable -> (diameter, squarings, refinements). Small inputs only (pure-Python loop)."""
+    def same(x: Csr, y: Csr):
+        xr, xc, _ = x.arrays()
+        yr, yc, _ = y.arrays()
+        return x.nnz == y.nnz and np.array_equal(xr, yr) and np.array_equal(xc, yc)
+    r0 = add(a, identity(a.n, a.dtype))
+    current, reach, prev_saved, prev_reach, sq = r0, 1, r0, 0, 0
+    while True:
+        nxt = matmul_seq(current, current)
+        sq += 1
+        if same(nxt, current):
+            break
+        prev_saved, prev_reach, current, reach = current, reach, nxt, reach * 2
+    if prev_reach == 0:
+        return 1, sq, 0
+    refine, d, rf = prev_saved, prev_reach, 0
+    while True:
+        nxt = matmul_seq(refine, r0)
+        d += 1
+        rf += 1
+        if same(nxt, refine):
+            return d - 1, sq, rf
+        refine = nxt
+
+
 def rcm_order(a: Csr) -> np.ndarray:
     """The order CsrMatrix::rcm (src/graph_csr.rs:663-722) permutes by (perm[new] = old)."""
     out = np.empty(max(a.n, 1), np.uint32)

@@ -27,6 +27,12 @@ using namespace slat;
 // max(B) for the CSR walk too (SLAT_NO_NARROW_CSR=1: the u64 slots of before, for A/B runs)
 static const bool kNarrowCsr = std::getenv("SLAT_NO_NARROW_CSR") == nullptr;
 static void dev_release_all(slat_ctx *ctx);
+// slat_fat.hip: the fat-row category (a workgroup and a dense LDS accumulator per row)
+namespace slat { struct FatArgs; }
+size_t slat_fat_ws(uint64_t n);
+slat_status slat_fat_select(slat_ctx *ctx, slat::Args &a, void *ws, slat::FatArgs *out);
+slat_status slat_fat_symbolic(slat_ctx *ctx, slat::FatArgs &f, const slat::Args &a, bool idx32);
+slat_status slat_fat_numeric(slat_ctx *ctx, slat::FatArgs &f, const slat::Args &a, int32_t dtype, bool f64any, bool idx32);
 
 extern "C" {
 
@@ -629,7 +635,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.stats = (flags & SLAT_FLAG_STATS) ? 1u : 0u;
 
     // 32-bit offsets whenever every position fits (the common case; halves the index math)
-    const bool idx32 = A->nnz < 0xFFFFFFFFull && B->nnz < 0xFFFFFFFFull;
+    const bool idx32 = A->nnz < 0xFFFFFFFFull && B->nnz < 0xFFFFFFFFull && !(flags & SLAT_FLAG_IDX64);
     uint32_t ablate = 0;  // experiments only: never reaches the real pipeline's kernels
     if (const char *e_ = std::getenv("SLAT_ABLATE")) ablate = (uint32_t)std::atoi(e_);
     Args asym = a;
@@ -711,7 +717,13 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // | their counters
     const size_t o_rb = o_smask + smask_b, rb_b = sym_batched ? up256(n * 4) : 0;
     const size_t o_l1 = o_rb + rb_b, o_l2 = o_l1 + rb_b, o_lc = o_l2 + rb_b, lc_b = sym_batched ? 256 : 0;
-    if ((st = slat_ensure_ws(ctx, o_lc + lc_b))) return st;
+    // fat rows (MAGNUS's dense-accumulation category) once a row can reach kFat products:
+    // max row of A x max row of B (A's max row unknown: when B has long rows)
+    static const bool kNoFat = std::getenv("SLAT_NO_FAT") != nullptr;
+    const uint64_t maxrow_a = A->max_row_nnz;
+    const bool fat = !kNoFat && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
+    const size_t o_fat = o_lc + lc_b, fat_b = fat ? slat_fat_ws(n) : 0;
+    if ((st = slat_ensure_ws(ctx, o_fat + fat_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (ell) {
         a.ell_wq = (uint32_t)wq;
@@ -792,6 +804,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                            a.epoch);
         SLAT_HIP(ctx, hipGetLastError());
     }
+    alignas(16) uint8_t fat_store[1024];
+    slat::FatArgs *fa = (slat::FatArgs *)fat_store;
+    if (fat) {
+        if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return st;
+        asym.fr_mark = a.fr_mark;
+    }
     if (ablate & 7u) {
         // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded
         Args abl = asym;
@@ -803,6 +821,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
     }
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
+    if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return st;
     if (sym_batched) {
         // MAGNUS categorisation: product bound per row, then the short rows batched in hash tables
         // (listing the rest), then the listed rows by windows
@@ -885,6 +904,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, he);
     }
     SLAT_HIP(ctx, launch_num(a));
+    if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return st;
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
     if (a.stats) SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                              hipMemcpyDeviceToHost, s));

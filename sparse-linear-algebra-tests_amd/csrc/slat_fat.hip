@@ -1,0 +1,414 @@
+// slat_fat.hip — the fat-row category of the SpGEMM (MAGNUS's dense accumulation for rows whose
+// products outgrow a wavefront's LDS slots), SURVEY.md §8(a) row a7.
+//
+// A row of C = A·B with many products (power-law hubs, dense powers of a graph: thousands of
+// outputs per row) would take the wavefront kernels many rank chunks or column windows, each a full
+// re-walk of the row. Here such rows get a workgroup of 512 threads and the whole 160 KB LDS:
+//
+//   k_fr_select   one thread per row: products = sum over the row's entries k of nnz(B row k),
+//                 cut off at kFat; rows at or above it are marked (the other kernels skip them)
+//                 and listed.
+//   k_fr_symbolic one block per listed row: a column bitmap over 2^20 columns per pass (128 KB),
+//                 one bit per product, popcount -> the row's structural count; also the mask of
+//                 touched accumulator chunks, so the numeric pass visits only those.
+//   k_fr_numeric  one block per listed row, per touched chunk of kChunk columns: a dense LDS
+//                 accumulator indexed by column (no hash, no ranks), a bitmap of touched columns,
+//                 then the emit: a block scan of the words' popcounts gives every column its
+//                 position, so the row comes out sorted (the reference sorts nz_cols,
+//                 src/graph_csr.rs:331,449). Integer semirings and f64 in any order add with LDS
+//                 atomics, lanes spread over the row's A entries (a long B row is walked by the
+//                 whole wave). f64 in the reference's order (the left fold of linalg/src/csr.rs:
+//                 325-337) gives each wave its own slice of the chunk's columns and walks the A
+//                 entries in order, lanes over one B row: one writer per column, in A order.
+//
+// B is read in its CSR form; the B-row part inside a column range is found by a 64-ary search.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+
+#include "slat.h"
+#include "slat_internal.hpp"
+#include "spgemm_kernels.hpp"
+
+namespace slat {
+
+constexpr int kFB = 512;                 // threads per fat-row block
+constexpr int kFW = kFB / kWave;         // waves per block
+constexpr uint64_t kFat = 16384;         // products per row from which a row is fat
+constexpr uint32_t kSymBits = 1u << 20;  // symbolic bitmap columns per pass (128 KB)
+
+// columns per accumulator chunk: 128 KB of V slots + the chunk's bitmap
+template <typename Sem>
+__host__ __device__ constexpr uint32_t fr_chunk() {
+    return (128u * 1024u) / (uint32_t)(sizeof(typename Sem::V) * Sem::kSlots);
+}
+template <typename Sem>
+__host__ __device__ constexpr size_t fr_lds() {
+    return (size_t)fr_chunk<Sem>() * sizeof(typename Sem::V) * Sem::kSlots + fr_chunk<Sem>() / 8 + 64 * 8;
+}
+
+__device__ __forceinline__ uint32_t cap63(uint64_t x) { return x < 63 ? (uint32_t)x : 63u; }
+
+struct FatArgs {
+    Args a;
+    uint32_t *list;          // fat rows
+    unsigned int *cnt;       // their number
+    uint8_t *mark;           // [n] 1 = fat
+    unsigned long long *cmask;  // [list position] touched accumulator chunks (bit c: chunk c; 64 max)
+    uint32_t csh;            // log2 of the chunk mask's granule (columns per mask bit)
+};
+
+static_assert(sizeof(FatArgs) <= 1024, "slat_api.hip keeps FatArgs in a 1 KB buffer");
+
+// products of each row, cut off at kFat; fat rows marked and listed
+__global__ __launch_bounds__(kBlock) void k_fr_select(FatArgs f) {
+    const Args &p = f.a;
+    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r - threadIdx.x < p.nrows;
+         r += (uint64_t)gridDim.x * kBlock) {
+        bool fat = false;
+        if (r < p.nrows) {
+            uint64_t fl = 0;
+            for (uint64_t i = p.a_rp[r], e = p.a_rp[r + 1]; i < e && fl < kFat; ++i) {
+                const uint32_t k = p.a_col[i];
+                if (k < p.b_nrows) fl += p.b_rp[k + 1] - p.b_rp[k];
+            }
+            fat = fl >= kFat;
+            f.mark[r] = fat ? 1 : 0;
+        }
+        const unsigned long long m = __ballot(fat);
+        if (m) {
+            unsigned int base = 0;
+            if (lane_id() == 0) base = atomicAdd(f.cnt, (unsigned int)__popcll(m));
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (fat) f.list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)r;
+        }
+    }
+}
+
+// [s, e) = the entries of B row [bs, be) with columns in [lo, hi), by the whole wave: a 64-ary
+// search (64 pivots per round, one per lane) while the range is longer than a wave
+template <typename I>
+__device__ __forceinline__ void b_range(const uint32_t *bcol, I bs, I be, uint32_t lo, uint32_t hi, I &s, I &e) {
+    const int lane = lane_id();
+    auto lower = [&](uint32_t key) -> I {  // first index in [bs, be) with col >= key
+        I a = bs, b = be;
+        while (b - a > (I)kWave) {
+            const I step = (b - a + (I)kWave - 1) / (I)kWave;
+            const I at = a + (I)lane * step;
+            const bool below = at < b && bcol[at] < key;
+            const uint32_t nb = __popcll(__ballot(below));  // pivots below key: a prefix of lanes
+            const I na = nb ? a + (I)(nb - 1) * step + 1 : a;
+            const I nbd = min(b, a + (I)nb * step + 1);
+            a = na;
+            b = nbd;
+        }
+        const I at = a + (I)lane;
+        const bool below = at < b && bcol[at] < key;
+        return a + (I)__popcll(__ballot(below));
+    };
+    s = lo == 0 ? bs : lower(lo);
+    e = lower(hi);
+}
+
+// every product (column j, value a*b) of A row [a0, a1) with j in [lo, hi), by one block: lanes over
+// the A entries (a B row of at most kLongB entries walked by its lane, a longer one by the wave);
+// fn(j, a, bidx) with bidx the B entry (values loaded by the caller only when needed)
+template <typename I, typename F>
+__device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, uint32_t hi, bool all_cols, F &&fn) {
+    const int lane = lane_id();
+    const int wv = threadIdx.x / kWave;
+    for (I base = a0 + (I)wv * kWave; base < a1; base += (I)kFB) {
+        const I i = base + (I)lane;
+        uint32_t k = kSent;
+        if (i < a1) k = p.a_col[i];
+        if (k >= p.b_nrows) k = kSent;
+        I bs = 0, be = 0;
+        if (k != kSent) {
+            bs = (I)p.b_rp[k];
+            be = (I)p.b_rp[k + 1];
+        }
+        const bool lng = (uint64_t)(be - bs) > kLongB;
+        if (!lng)
+            for (I j = bs; j < be; ++j) {
+                const uint32_t c = p.b_col[j];
+                if (all_cols || (c >= lo && c < hi)) fn(c, i, j);
+            }
+        for (unsigned long long m = __ballot(lng); m; m &= m - 1) {
+            const int l = (int)__builtin_ctzll(m);
+            const I s0 = (I)readlane_u64((uint64_t)bs, l), e0 = (I)readlane_u64((uint64_t)be, l);
+            const I ia = (I)readlane_u64((uint64_t)i, l);
+            I s = s0, e = e0;
+            if (!all_cols) b_range<I>(p.b_col, s0, e0, lo, hi, s, e);
+            for (I j = s + (I)lane; j < e; j += (I)kWave) fn(p.b_col[j], ia, j);
+        }
+    }
+}
+
+// block-wide exclusive scan of one u32 per thread (512 threads); returns the block total via *tot
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sh, uint32_t &tot) {
+    const int lane = lane_id(), wv = threadIdx.x / kWave;
+    const uint32_t incl = wave_incl_scan(v, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    if (lane == kWave - 1) sh[wv] = incl;
+    __syncthreads();
+    uint32_t pre = 0;
+    tot = 0;
+#pragma unroll
+    for (int w = 0; w < kFW; ++w) {
+        const uint32_t x = sh[w];
+        pre += w < wv ? x : 0u;
+        tot += x;
+    }
+    __syncthreads();
+    return pre + incl - v;
+}
+
+template <typename I>
+__global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
+    const Args &p = f.a;
+    constexpr uint32_t kWords = kSymBits / 32;
+    // dynamic LDS only (16-byte aligned carve): bitmap | block-scan words | chunk-mask words
+    extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
+    uint32_t *sh = bits + kWords;
+    unsigned long long *shm = (unsigned long long *)(bits + kWords + kFW);
+    const unsigned int nl = *(volatile unsigned int *)f.cnt;
+    for (uint32_t w = threadIdx.x; w < kWords; w += kFB) bits[w] = 0;
+    __syncthreads();
+    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const uint64_t row = f.list[li];
+        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
+        uint64_t count = 0;
+        unsigned long long cm = 0;
+        for (uint64_t lo = 0; lo < p.ncols; lo += kSymBits) {
+            const uint32_t hi = (uint32_t)min<uint64_t>(p.ncols, lo + kSymBits);
+            const bool all = lo == 0 && hi == p.ncols;
+            fr_walk<I>(p, a0, a1, (uint32_t)lo, hi, all, [&](uint32_t c, I, I) {
+                const uint32_t o = c - (uint32_t)lo;
+                atomicOr(&bits[o >> 5], 1u << (o & 31));
+            });
+            __syncthreads();
+            uint32_t pc = 0;
+            for (uint32_t w = threadIdx.x; w < kWords; w += kFB) {
+                const uint32_t x = bits[w];
+                if (x) {
+                    pc += __popc(x);
+                    cm |= 1ull << cap63((lo + (uint64_t)w * 32) >> f.csh);
+                    bits[w] = 0;
+                }
+            }
+            uint32_t tot;
+            (void)block_excl_scan(pc, sh, tot);
+            count += tot;
+        }
+        // the touched-chunk mask: OR over the block
+        cm = readlane_u64(wave_or_u32((uint32_t)cm) | ((uint64_t)wave_or_u32((uint32_t)(cm >> 32)) << 32), 0);
+        if (lane_id() == 0) shm[threadIdx.x / kWave] = cm;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long all = 0;
+            for (int w = 0; w < kFW; ++w) all |= shm[w];
+            f.cmask[li] = all;
+            p.counts[row] = count;
+        }
+        __syncthreads();
+    }
+}
+
+// The chunk's products into the dense accumulator. Integer semirings / f64 any order: LDS atomics,
+// lanes over A entries. f64 in the reference's order: wave w owns columns [c0 + w*span, ...) and
+// walks the A entries in order, lanes over one B row (distinct columns): one writer per column.
+template <typename Sem, typename I>
+__device__ __forceinline__ void fr_accumulate(const Args &p, I a0, I a1, uint32_t c0, uint32_t c1,
+                                              typename Sem::V *acc, uint32_t *bits) {
+    using S = typename Sem::S;
+    const S *av = (const S *)p.a_val;
+    const S *bv = (const S *)p.b_val;
+    if constexpr (!Sem::kOrdered) {
+        const bool all = c0 == 0 && c1 == p.ncols;
+        fr_walk<I>(p, a0, a1, c0, c1, all, [&](uint32_t c, I ia, I jb) {
+            const uint32_t o = c - c0;
+            Sem::acc(acc, o, Sem::prod(av[ia], bv[jb]));
+            atomicOr(&bits[o >> 5], 1u << (o & 31));
+        });
+    } else {
+        const int lane = lane_id(), wv = threadIdx.x / kWave;
+        const uint32_t span = (c1 - c0 + kFW - 1) / kFW;
+        const uint32_t lo = c0 + (uint32_t)wv * span, hi = min(c1, lo + span);
+        if (lo >= hi) return;
+        for (I base = a0; base < a1; base += (I)kWave) {
+            const I i = base + (I)lane;
+            uint32_t k = kSent;
+            S a = S(0);
+            I bs = 0, be = 0;
+            if (i < a1) {
+                k = p.a_col[i];
+                a = av[i];
+                if (k < p.b_nrows) {
+                    bs = (I)p.b_rp[k];
+                    be = (I)p.b_rp[k + 1];
+                }
+            }
+            const int cnt = (int)min<uint64_t>((uint64_t)kWave, (uint64_t)(a1 - base));
+            for (int t = 0; t < cnt; ++t) {  // A entries in order: the left fold
+                const I s0 = (I)readlane_u64((uint64_t)bs, t), e0 = (I)readlane_u64((uint64_t)be, t);
+                if (s0 == e0) continue;
+                const S at = readlane_val(a, t);
+                I s, e;
+                b_range<I>(p.b_col, s0, e0, lo, hi, s, e);
+                for (I j = s + (I)lane; j < e; j += (I)kWave) {
+                    const uint32_t o = p.b_col[j] - c0;
+                    acc[o] = __dadd_rn(acc[o], __dmul_rn(at, bv[j]));
+                    atomicOr(&bits[o >> 5], 1u << (o & 31));
+                }
+                wave_sync();  // this entry's adds land before the next entry's (same columns)
+            }
+        }
+    }
+}
+
+template <typename Sem, typename I>
+__global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
+    using S = typename Sem::S;
+    using V = typename Sem::V;
+    const Args &p = f.a;
+    constexpr uint32_t CH = fr_chunk<Sem>();
+    constexpr uint32_t kWords = CH / 32;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    V *acc = (V *)smem;
+    uint32_t *bits = (uint32_t *)(smem + (size_t)CH * sizeof(V) * Sem::kSlots);
+    uint32_t *sh = bits + kWords;
+    for (uint32_t w = threadIdx.x; w < CH * Sem::kSlots; w += kFB) acc[w] = V(0);
+    for (uint32_t w = threadIdx.x; w < kWords; w += kFB) bits[w] = 0;
+    __syncthreads();
+    S *cval = (S *)p.c_val;
+    const unsigned int nl = *(volatile unsigned int *)f.cnt;
+    uint32_t zrows = 0;
+    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const uint64_t row = f.list[li];
+        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
+        const uint64_t ob = p.c_rp[row], oe = p.c_rp[row + 1];
+        const unsigned long long cm = f.cmask[li];
+        uint64_t pos = 0;
+        uint32_t zeros = 0;
+        for (uint64_t c0 = 0; c0 < p.ncols; c0 += CH) {
+            // skip chunks with no product (mask granule 2^csh columns, a multiple of CH or the last)
+            if (!((cm >> cap63(c0 >> f.csh)) & 1ull)) continue;
+            const uint32_t c1 = (uint32_t)min<uint64_t>(p.ncols, c0 + CH);
+            fr_accumulate<Sem, I>(p, a0, a1, (uint32_t)c0, c1, acc, bits);
+            __syncthreads();
+            // emit: thread t owns bitmap word t (32 columns); positions by a block scan
+            uint32_t x = 0;
+            if (threadIdx.x < kWords) x = bits[threadIdx.x];
+            uint32_t tot;
+            const uint32_t pre = block_excl_scan(__popc(x), sh, tot);
+            uint32_t q = 0;
+            for (uint32_t m = x; m; m &= m - 1, ++q) {
+                const uint32_t o = threadIdx.x * 32 + (uint32_t)__builtin_ctz(m);
+                S v = Sem::finish(acc, o);
+#pragma unroll
+                for (int w = 0; w < Sem::kSlots; ++w) acc[o * Sem::kSlots + w] = V(0);
+                zeros += Sem::is_zero(v) ? 1u : 0u;
+                const uint64_t at = ob + pos + pre + q;
+                if (at < oe) {  // never write past the row's slice
+                    p.c_col[at] = (uint32_t)c0 + o;
+                    cval[at] = v;
+                }
+            }
+            if (threadIdx.x < kWords) bits[threadIdx.x] = 0;
+            pos += tot;
+            __syncthreads();
+        }
+        uint32_t zt;
+        (void)block_excl_scan(zeros, sh, zt);
+        if (threadIdx.x == 0) {
+            p.counts[row] = pos - zt;
+            zrows += zt ? 1u : 0u;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && zrows)
+        __hip_atomic_fetch_add(&p.host_out[2], (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace slat
+
+using namespace slat;
+
+// workspace bytes of the fat-row category for n rows
+size_t slat_fat_ws(uint64_t n) { return ((n + 255) & ~255ull) * (1 + 4 + 8) + 256; }
+
+// Select the fat rows (marks into a.fr_mark's buffer) and count them on the device; nothing to do on
+// the host. `ws` = slat_fat_ws(n) bytes of workspace.
+slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
+    const hipStream_t s = ctx->stream;
+    const uint64_t n = a.nrows;
+    const uint64_t nn = (n + 255) & ~255ull;
+    uint8_t *w = (uint8_t *)ws;
+    FatArgs f;
+    f.mark = w;
+    f.list = (uint32_t *)(w + nn);
+    f.cmask = (unsigned long long *)(w + nn * 5);
+    f.cnt = (unsigned int *)(w + nn * 13);
+    // the chunk mask's granule: at least the largest accumulator chunk (2^14 columns), at most 64
+    // granules over the columns
+    uint32_t csh = 14;
+    while (csh < 63 && (a.ncols >> csh) > 63) ++csh;
+    f.csh = csh;
+    SLAT_HIP(ctx, hipMemsetAsync(f.cnt, 0, 4, s));
+    a.fr_mark = f.mark;
+    f.a = a;
+    const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 8));
+    hipLaunchKernelGGL(k_fr_select, dim3(g), dim3(kBlock), 0, s, f);
+    SLAT_HIP(ctx, hipGetLastError());
+    *out = f;
+    return SLAT_OK;
+}
+
+slat_status slat_fat_symbolic(slat_ctx *ctx, FatArgs &f, const Args &a, bool idx32) {
+    f.a = a;
+    const dim3 g((unsigned)ctx->cu_count);
+    const size_t lds = kSymBits / 8 + kFW * 4 + kFW * 8;
+    static bool attr = false;
+    if (!attr) {  // more than 64 KB of dynamic LDS per block
+        (void)hipFuncSetAttribute((const void *)k_fr_symbolic<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void *)k_fr_symbolic<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    if (idx32)
+        hipLaunchKernelGGL(k_fr_symbolic<uint32_t>, g, dim3(kFB), lds, ctx->stream, f);
+    else
+        hipLaunchKernelGGL(k_fr_symbolic<uint64_t>, g, dim3(kFB), lds, ctx->stream, f);
+    SLAT_HIP(ctx, hipGetLastError());
+    return SLAT_OK;
+}
+
+template <typename Sem>
+static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
+    const dim3 g((unsigned)ctx->cu_count);
+    const size_t lds = fr_lds<Sem>();
+    // the chunk mask's granule must be a multiple of this instance's chunk
+    FatArgs h = f;
+    if ((1ull << h.csh) < fr_chunk<Sem>()) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {  // more than 64 KB of dynamic LDS per block
+        (void)hipFuncSetAttribute((const void *)k_fr_numeric<Sem, uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void *)k_fr_numeric<Sem, uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr = true;
+    }
+    if (idx32)
+        hipLaunchKernelGGL((k_fr_numeric<Sem, uint32_t>), g, dim3(kFB), lds, ctx->stream, h);
+    else
+        hipLaunchKernelGGL((k_fr_numeric<Sem, uint64_t>), g, dim3(kFB), lds, ctx->stream, h);
+    return hipGetLastError();
+}
+
+slat_status slat_fat_numeric(slat_ctx *ctx, FatArgs &f, const Args &a, int32_t dtype, bool f64any, bool idx32) {
+    f.a = a;
+    hipError_t e;
+    if (dtype == SLAT_U32) e = fr_num<SemU32>(ctx, f, idx32);
+    else if (dtype == SLAT_SAT64) e = fr_num<SemSat64>(ctx, f, idx32);
+    else if (f64any) e = fr_num<SemF64Any>(ctx, f, idx32);
+    else e = fr_num<SemF64>(ctx, f, idx32);
+    SLAT_HIP(ctx, e);
+    return SLAT_OK;
+}

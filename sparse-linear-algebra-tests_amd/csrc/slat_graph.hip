@@ -270,3 +270,87 @@ extern "C" slat_status slat_connected_components(slat_ctx *ctx, const slat_csr_v
     if (e != hipSuccess) return fail(ctx, SLAT_EHIP, std::string("connected_components: ") + hipGetErrorString(e));
     return SLAT_OK;
 }
+
+// bench_diameter's algorithm (src/graph_csr.rs:1228-1319) as a device-resident driver: R0 = A + I of
+// the undirected graph (R[i][j] > 0 iff dist(i, j) <= 1); phase 1 squares until the pattern stops
+// changing (reach doubles each time), phase 2 multiplies the last power before stabilisation by R0
+// until its pattern stops changing. Loop decisions (pattern equality) are the only host round trips.
+extern "C" slat_status slat_diameter(slat_ctx *ctx, const slat_csr_view *A, uint64_t *diameter, uint64_t *squarings,
+                                     uint64_t *refinements) {
+    if (!ctx || !diameter) return SLAT_EINVAL;
+    slat_status st = square_check(ctx, A);
+    if (st) return st;
+    slat_csr id = {}, r0 = {};
+    if ((st = slat_csr_identity(ctx, A->n_rows, A->dtype, &id))) return st;
+    slat_csr_view vi = slat_csr_view_of(&id);
+    st = slat_csr_add(ctx, A, &vi, &r0);
+    slat_csr_free(ctx, &id);
+    if (st) return st;
+    slat_csr_view vr0 = slat_csr_view_of(&r0);
+    uint64_t sq = 0, rf = 0, prev_reach = 0, reach = 1;
+    slat_csr current = {}, prev_saved = {};
+    if ((st = slat_csr_create(ctx, &vr0, &current))) {
+        slat_csr_free(ctx, &r0);
+        return st;
+    }
+    auto cleanup = [&]() {
+        if (current.row_ptr) slat_csr_free(ctx, &current);
+        if (prev_saved.row_ptr) slat_csr_free(ctx, &prev_saved);
+        slat_csr_free(ctx, &r0);
+    };
+    for (;;) {  // phase 1: repeated squaring
+        slat_csr next = {};
+        slat_csr_view vc = slat_csr_view_of(&current);
+        if ((st = slat_spgemm(ctx, &vc, &vc, &next, 0))) break;
+        ++sq;
+        slat_csr_view vn = slat_csr_view_of(&next);
+        int32_t eq = 0;
+        if ((st = slat_csr_pattern_equal(ctx, &vn, &vc, &eq))) {
+            slat_csr_free(ctx, &next);
+            break;
+        }
+        if (eq) {  // stabilised: diameter in (prev_reach, 2 * reach]
+            slat_csr_free(ctx, &next);
+            break;
+        }
+        if (prev_saved.row_ptr) slat_csr_free(ctx, &prev_saved);
+        prev_saved = current;
+        prev_reach = reach;
+        current = next;
+        reach *= 2;
+    }
+    if (st) {
+        cleanup();
+        return st;
+    }
+    uint64_t d = 1;  // stabilised on the first squaring: R0 is its own closure (diameter <= 1)
+    if (prev_reach != 0) {  // phase 2: linear refinement from the power covering <= prev_reach
+        slat_csr refine = prev_saved;
+        prev_saved = {};
+        d = prev_reach;
+        for (;;) {
+            slat_csr next = {};
+            slat_csr_view vf = slat_csr_view_of(&refine);
+            if ((st = slat_spgemm(ctx, &vf, &vr0, &next, 0))) break;
+            ++rf;
+            ++d;
+            slat_csr_view vn = slat_csr_view_of(&next);
+            int32_t eq = 0;
+            st = slat_csr_pattern_equal(ctx, &vn, &vf, &eq);
+            slat_csr_free(ctx, &refine);
+            refine = next;
+            if (st) break;
+            if (eq) {
+                d -= 1;
+                break;
+            }
+        }
+        slat_csr_free(ctx, &refine);
+    }
+    cleanup();
+    if (st) return st;
+    *diameter = d;
+    if (squarings) *squarings = sq;
+    if (refinements) *refinements = rf;
+    return SLAT_OK;
+}

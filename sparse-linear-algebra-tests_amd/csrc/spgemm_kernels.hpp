@@ -5,7 +5,7 @@
 //
 // Pipeline (the reference's matmul_par structure, src/graph_csr.rs:360-476, re-designed):
 //   k_symbolic  one wavefront per row: structural nnz via an LDS column bitmap
-//   (scan)      hipcub inclusive scan -> C.row_ptr
+//   k_scan_rows single-pass decoupled look-back scan -> C.row_ptr
 //   k_numeric   one row GROUP (1 or 4 wavefronts) per row:
 //                 1. gather: every scalar product (j, a_ik*b_kj) of the row, loaded with batched
 //                    independent loads (Q A-entries x U B-entries per lane in flight), into an LDS
@@ -110,7 +110,12 @@ struct Args {
     uint32_t *c_col;
     void *c_val;
     unsigned long long *shards;
+    // rows of the fat-row category (slat_fat.hip: a workgroup and a dense LDS accumulator per row),
+    // which the kernels here skip; null = none
+    const uint8_t *fr_mark;
 };
+
+__device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.fr_mark && p.fr_mark[row]; }
 
 // ------------------------------------------------------------------------------------------------
 // value semirings: S storage type, P cached product, V LDS accumulator
@@ -1193,6 +1198,7 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
+        if (fat_row(p, row)) continue;  // the fat-row kernels' row
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         if constexpr (MODE != 0) {
             if (!listed && sym_short_row((uint64_t)(a1 - a0), p.b_maxrow) != (MODE == 1)) continue;  // the other launch's row
@@ -1337,6 +1343,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
+        if (fat_row(p, row)) continue;  // the fat-row kernels' row
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         const uint64_t out_begin = p.c_rp[row], out_end = p.c_rp[row + 1];
         uint64_t out_pos = out_begin;
@@ -1717,9 +1724,10 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
             bj = p.rbound[r];
         }
         const uint64_t lj = A1j - A0j;
-        const bool shortj = (uint32_t)lane < nt && bj <= kCap && lj <= 256;
+        const bool fatj = (uint32_t)lane < nt && fat_row(p, r);
+        const bool shortj = (uint32_t)lane < nt && bj <= kCap && lj <= 256 && !fatj;
         const unsigned long long shortm = __ballot(shortj);
-        list_rows(p, (uint32_t)lane < nt && !shortj, r);
+        list_rows(p, (uint32_t)lane < nt && !shortj && !fatj, r);
         uint32_t b = 0;
         for (;;) {
             const unsigned long long m = b < (uint32_t)kWave ? (shortm >> b) << b : 0ull;
@@ -1907,9 +1915,10 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
             oej = p.c_rp[r + 1];
         }
         const uint64_t uj = oej - obj, lj = A1j - A0j;
-        const bool shortj = (uint32_t)lane < nt && uj <= kHashT / 2;
+        const bool fatj = (uint32_t)lane < nt && fat_row(p, r);
+        const bool shortj = (uint32_t)lane < nt && uj <= kHashT / 2 && !fatj;
         const unsigned long long shortm = __ballot(shortj);
-        list_rows(p, (uint32_t)lane < nt && !shortj, r);  // the window launch's rows
+        list_rows(p, (uint32_t)lane < nt && !shortj && !fatj, r);  // the window launch's rows
         uint32_t b = 0;
         for (;;) {
             const unsigned long long m = b < (uint32_t)kWave ? (shortm >> b) << b : 0ull;

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("SLAT_LIB_PATH") or os.path.join(PKG_DIR, "libslat.so"
 SLAT_OK, SLAT_EINVAL, SLAT_EDIM, SLAT_EOOM, SLAT_EHIP, SLAT_ENOTSUP, SLAT_ENODEV = range(7)
 U32, SAT64, F64 = 0, 1, 2
 DEVICE, HOST = 0, 1
-FLAG_TIMING, FLAG_EXACT_ALLOC, FLAG_STATS, FLAG_F64_ANY_ORDER = 0x1, 0x2, 0x4, 0x8
+FLAG_TIMING, FLAG_EXACT_ALLOC, FLAG_STATS, FLAG_F64_ANY_ORDER, FLAG_IDX64 = 0x1, 0x2, 0x4, 0x8, 0x10
 
 # Every symbol include/slat.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -29,7 +29,7 @@ EXPORTS = [
     "slat_bandwidth_stats", "slat_spgemm_dense", "slat_device_alloc", "slat_device_free", "slat_device_copy",
     "slat_magnus_matmul", "slat_magnus_free", "slat_magnus_to_host", "slat_magnus_view_of",
     "slat_comm_id", "slat_comm_create", "slat_comm_destroy", "slat_rowblock_cuts", "slat_bcast_csr",
-    "slat_allgather_rows",
+    "slat_allgather_rows", "slat_diameter",
 ]
 
 
@@ -160,6 +160,7 @@ def lib():
         "slat_rowblock_cuts": ([vp, P(CsrView), P(CsrView), u32, vp], C.c_int),
         "slat_bcast_csr": ([vp, vp, P(CsrOwned), C.c_int], C.c_int),
         "slat_allgather_rows": ([vp, vp, P(CsrView), P(CsrOwned)], C.c_int),
+        "slat_diameter": ([vp, P(CsrView), P(u64), P(u64), P(u64)], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -491,6 +491,13 @@ class DeviceCsr:
         L.check(L.lib().slat_connected_components(self._ctx.ptr, C.byref(a), comp.ctypes.data), self._ctx.ptr)
         return comp[:self.n].tolist()
 
+    def diameter(self):
+        """bench_diameter (src/graph_csr.rs:1228-1319) on this undirected graph, device-resident:
+        -> (diameter, squarings, refinements)."""
+        a, d, sq, rf = self.view(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+        L.check(L.lib().slat_diameter(self._ctx.ptr, C.byref(a), C.byref(d), C.byref(sq), C.byref(rf)), self._ctx.ptr)
+        return int(d.value), int(sq.value), int(rf.value)
+
     def clone(self):
         """`Clone` of the owned matrix: a device-to-device copy."""
         v = self.view()
