@@ -111,36 +111,74 @@ __device__ __forceinline__ void b_range(const uint32_t *bcol, I bs, I be, uint32
     e = lower(hi);
 }
 
-// every product (column j, value a*b) of A row [a0, a1) with j in [lo, hi), by one block: lanes over
-// the A entries (a B row of at most kLongB entries walked by its lane, a longer one by the wave);
-// fn(j, a, bidx) with bidx the B entry (values loaded by the caller only when needed)
-template <typename I, typename F>
+// every product of A row [a0, a1) with column j in [lo, hi), by one block: fn(j, a, b) with the A and
+// B values (VALS; else zeros). Lanes take kQ A entries at a time (their B-row bounds loaded together);
+// a B row of at most kLongB entries is walked by its lane, two entries per step for all kQ rows at
+// once (2 kQ independent loads in flight), a longer one by the whole wave over its part in [lo, hi).
+constexpr int kQ = 4;
+template <typename S, bool VALS, typename I, typename F>
 __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, uint32_t hi, bool all_cols, F &&fn) {
     const int lane = lane_id();
     const int wv = threadIdx.x / kWave;
-    for (I base = a0 + (I)wv * kWave; base < a1; base += (I)kFB) {
-        const I i = base + (I)lane;
-        uint32_t k = kSent;
-        if (i < a1) k = p.a_col[i];
-        if (k >= p.b_nrows) k = kSent;
-        I bs = 0, be = 0;
-        if (k != kSent) {
-            bs = (I)p.b_rp[k];
-            be = (I)p.b_rp[k + 1];
-        }
-        const bool lng = (uint64_t)(be - bs) > kLongB;
-        if (!lng)
-            for (I j = bs; j < be; ++j) {
-                const uint32_t c = p.b_col[j];
-                if (all_cols || (c >= lo && c < hi)) fn(c, i, j);
+    const S *av = (const S *)p.a_val;
+    const S *bv = (const S *)p.b_val;
+    for (I base = a0 + (I)wv * kWave; base < a1; base += (I)kFB * kQ) {
+        uint32_t k[kQ];
+        S a[kQ];
+        I bs[kQ], be[kQ];
+        sfor<kQ>([&](auto Q) {
+            const I i = base + (I)(Q * kFB) + (I)lane;
+            k[Q] = kSent;
+            a[Q] = S(0);
+            if (i < a1) {
+                k[Q] = p.a_col[i];
+                if constexpr (VALS) a[Q] = av[i];
             }
-        for (unsigned long long m = __ballot(lng); m; m &= m - 1) {
-            const int l = (int)__builtin_ctzll(m);
-            const I s0 = (I)readlane_u64((uint64_t)bs, l), e0 = (I)readlane_u64((uint64_t)be, l);
-            const I ia = (I)readlane_u64((uint64_t)i, l);
-            I s = s0, e = e0;
-            if (!all_cols) b_range<I>(p.b_col, s0, e0, lo, hi, s, e);
-            for (I j = s + (I)lane; j < e; j += (I)kWave) fn(p.b_col[j], ia, j);
+        });
+        sfor<kQ>([&](auto Q) {
+            bs[Q] = be[Q] = 0;
+            if (k[Q] < p.b_nrows) {
+                bs[Q] = (I)p.b_rp[k[Q]];
+                be[Q] = (I)p.b_rp[k[Q] + 1];
+            }
+        });
+        uint32_t len[kQ], mx = 0;
+        sfor<kQ>([&](auto Q) {
+            const uint64_t l = (uint64_t)(be[Q] - bs[Q]);
+            len[Q] = l > kLongB ? 0u : (uint32_t)l;
+            mx = max(mx, len[Q]);
+            // a long B row: the whole wave over its part in [lo, hi)
+            for (unsigned long long m = __ballot(l > kLongB); m; m &= m - 1) {
+                const int l0 = (int)__builtin_ctzll(m);
+                const I s0 = (I)readlane_u64((uint64_t)bs[Q], l0), e0 = (I)readlane_u64((uint64_t)be[Q], l0);
+                const S at = readlane_val(a[Q], l0);
+                I s1 = s0, e1 = e0;
+                if (!all_cols) b_range<I>(p.b_col, s0, e0, lo, hi, s1, e1);
+                for (I j = s1 + (I)lane; j < e1; j += (I)kWave) fn(p.b_col[j], at, VALS ? bv[j] : S(0));
+            }
+        });
+        mx = wave_max_u32(mx);
+        for (uint32_t t = 0; t < mx; t += 2) {
+            uint32_t c[kQ][2];
+            S b[kQ][2];
+            sfor<kQ>([&](auto Q) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    c[Q][u] = kSent;
+                    b[Q][u] = S(0);
+                    if (t + u < len[Q]) {
+                        c[Q][u] = p.b_col[bs[Q] + (I)(t + u)];
+                        if constexpr (VALS) b[Q][u] = bv[bs[Q] + (I)(t + u)];
+                    }
+                }
+            });
+            sfor<kQ>([&](auto Q) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const uint32_t cc = c[Q][u];
+                    if (cc != kSent && (all_cols || (cc >= lo && cc < hi))) fn(cc, a[Q], b[Q][u]);
+                }
+            });
         }
     }
 }
@@ -182,7 +220,7 @@ __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
         for (uint64_t lo = 0; lo < p.ncols; lo += kSymBits) {
             const uint32_t hi = (uint32_t)min<uint64_t>(p.ncols, lo + kSymBits);
             const bool all = lo == 0 && hi == p.ncols;
-            fr_walk<I>(p, a0, a1, (uint32_t)lo, hi, all, [&](uint32_t c, I, I) {
+            fr_walk<uint32_t, false, I>(p, a0, a1, (uint32_t)lo, hi, all, [&](uint32_t c, uint32_t, uint32_t) {
                 const uint32_t o = c - (uint32_t)lo;
                 atomicOr(&bits[o >> 5], 1u << (o & 31));
             });
@@ -225,9 +263,9 @@ __device__ __forceinline__ void fr_accumulate(const Args &p, I a0, I a1, uint32_
     const S *bv = (const S *)p.b_val;
     if constexpr (!Sem::kOrdered) {
         const bool all = c0 == 0 && c1 == p.ncols;
-        fr_walk<I>(p, a0, a1, c0, c1, all, [&](uint32_t c, I ia, I jb) {
+        fr_walk<S, true, I>(p, a0, a1, c0, c1, all, [&](uint32_t c, S a, S b) {
             const uint32_t o = c - c0;
-            Sem::acc(acc, o, Sem::prod(av[ia], bv[jb]));
+            Sem::acc(acc, o, Sem::prod(a, b));
             atomicOr(&bits[o >> 5], 1u << (o & 31));
         });
     } else {

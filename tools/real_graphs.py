@@ -133,6 +133,21 @@ def chain(args, ctx):
             del result
             if nnz_out > MAX_NNZ:
                 break
+        if args.past_cap and prev.nnz() >= 0xFFFFFFFF:
+            # beyond the reference's protocol: one more product whose LEFT operand holds >= 2^32
+            # entries, so the 64-bit-offset kernels run (no timed repeat: memory)
+            t0 = time.perf_counter()
+            result = prev.matmul_par(A)
+            t_us = int((time.perf_counter() - t0) * 1e6)
+            rows = rng.choice(n, size=min(args.sample, n), replace=False)
+            got = dev_rows(result, rows)
+            want = exact_rows(dev_rows(prev, rows), ah)
+            ok = all(np.array_equal(g[0], w[0]) and np.array_equal(g[1], w[1]) for g, w in zip(got, want))
+            print(f"{name},{n},{len(s)},{step + 1} (past the cap: nnz(A^{step}) = {prev.nnz()}),{result.nnz()},{t_us},"
+                  f"{result.nnz() / max(t_us, 1) / 1e3:.3f},1,{ok}", flush=True)
+            if not ok:
+                raise AssertionError(f"{name} A^{step + 1}: GPU result differs")
+            del result
         del prev
 
 
@@ -187,6 +202,7 @@ def main():
     ap.add_argument("--rmat", nargs="*", default=["12:8", "17:8"], help="scale:degree of the synthetic graphs")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--iters", type=int, default=1)
+    ap.add_argument("--past-cap", action="store_true", help="chain: one more step after the 4.4e9 cap (idx64 left operand)")
     ap.add_argument("--sample", type=int, default=64, help="rows checked against the exact restatement per step")
     ap.add_argument("--check-full", type=float, default=2e5,
                     help="also compare whole products with the oracle while nnz(A) is at most this")
