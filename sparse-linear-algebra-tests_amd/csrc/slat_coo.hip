@@ -265,9 +265,12 @@ slat_status from_coo_dev(slat_ctx *ctx, uint64_t n, uint64_t nt, const uint32_t 
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     int endbit = 33;
     while (endbit < 64 && ((n + 1) >> (endbit - 32)) != 0) ++endbit;
-    // whole 8-bit digits: with a partial top digit the rocPRIM sort returned wrong orders above ~3M
-    // keys on this image (measured: 49-bit keys, 3.4M triplets)
-    endbit = std::min(64, (endbit + 7) & ~7);
+    // (Round 1 rounded endbit up to whole 8-bit digits after seeing wrong orders above ~3M keys. The
+    // cause was the stream-ordered pool's lost writes into a freshly grown block, which the scratch
+    // then came from: tools/repro/repro_pool.hip; the sort itself orders partial top digits correctly,
+    // tools/repro/repro_radix.cpp.)
+    // The sort takes an int item count (hipcub): 2^31 triplets or more would wrap negative.
+    if (nt >= 0x7FFFFFFFull) return fail(ctx, SLAT_ENOTSUP, "2^31 or more triplets (the radix sort's int count)");
     size_t sort_b = 0;
     SLAT_HIP(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (uint64_t *)nullptr, (uint64_t *)nullptr,
                                                      (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nt, 0, endbit, s));
@@ -275,7 +278,6 @@ slat_status from_coo_dev(slat_ctx *ctx, uint64_t n, uint64_t nt, const uint32_t 
                  o_up = o_h + up(nt * 8), o_uk = o_up + up((nt + 1) * 8), o_uv = o_uk + up(nt * 8),
                  o_kp = o_uv + up(nt * 8), o_fp = o_kp + up(nt * 8), o_rc = o_fp + up((nt + 1) * 8),
                  o_st = o_rc + up(n * 8), total_b = o_st + up(sort_b);
-    if (nt > 0xFFFFFFFFull) return fail(ctx, SLAT_ENOTSUP, "more than 2^32 triplets");
     Buf scratch{ctx};
     if (scratch.alloc(total_b) != hipSuccess) return fail(ctx, SLAT_EOOM, "from_coo scratch");
     uint8_t *w = (uint8_t *)scratch.p;
@@ -321,6 +323,7 @@ extern "C" slat_status slat_csr_from_coo(slat_ctx *ctx, uint64_t n, uint64_t ntr
     if (!ctx || !out || dtype < SLAT_U32 || dtype > SLAT_F64) return SLAT_EINVAL;
     if (ntrip && (!rows || !cols || !vals)) return fail(ctx, SLAT_EINVAL, "from_coo: null arrays");
     if (n > 0xFFFFFFFFull) return fail(ctx, SLAT_EINVAL, "n exceeds u32 ids");
+    if (ntrip >= 0x7FFFFFFFull) return fail(ctx, SLAT_ENOTSUP, "2^31 or more triplets (the radix sort's int count)");
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
     if (residency == SLAT_DEVICE) return from_coo_dev(ctx, n, ntrip, rows, cols, vals, dtype, out);
     // host triplets: one staging copy

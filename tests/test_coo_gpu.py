@@ -100,3 +100,17 @@ def test_generators_small_then_large_same_context(golden):
         h = b.host()
         assert_digest(digest(h.row_ptr, h.col_idx, h.values), golden["torus100_powers"][0], f"100^3 A rep {rep}")
         del b
+
+
+def test_from_coo_rejects_2_31_triplets():
+    """The device sort counts items in an int: 2^31 triplets or more -> SLAT_ENOTSUP before any device
+    work (a wrapped negative count would sort nothing)."""
+    import ctypes as C
+    ctx = slat.default_context(0)
+    buf = C.c_void_p()
+    slat.lib().slat_device_alloc(ctx.ptr, 4096, C.byref(buf))
+    out = slat._lib.CsrOwned()
+    for nt in (1 << 31, (1 << 32) - 1, 1 << 32):
+        rc = slat.lib().slat_csr_from_coo(ctx.ptr, 1000, nt, buf, buf, buf, slat.U32, slat.DEVICE, C.byref(out))
+        assert rc == 5, (nt, rc)  # SLAT_ENOTSUP
+    slat.lib().slat_device_free(ctx.ptr, buf)
