@@ -1339,7 +1339,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
     auto mark = [&](int i) { pc.mark(i); };
     uint64_t *ph = pc.ph;
-    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
+    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short / _sort
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
@@ -1350,7 +1350,9 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
         uint32_t zeros = 0;
         ph[kPhaseSlots - 1] += 1;
         if constexpr (MODE != 0) {
-            if ((out_end - out_begin <= kHashT / 2) != (MODE == 1)) continue;  // the other launch's row
+            // the other launch's row (listed rows are this launch's by construction: the sorted
+            // short-row category also lists rows with few outputs but > 256 entries or > 64 groups)
+            if (!listed && (out_end - out_begin <= kHashT / 2) != (MODE == 1)) continue;
         }
         if constexpr (MODE == 1) {
             // short row (its output count, known from symbolic, fits half the table)
@@ -1845,10 +1847,12 @@ __device__ __forceinline__ void batch_emit(uint32_t *hkeys, typename Sem::V *hva
             const uint32_t lr = cb ? k >> cb : 0u;
             const uint32_t ro = rowoff[lr], re = rowoff[lr + 1];
             uint32_t rk = 0;
+#ifndef SLAT_EXP_NORANK
             for (uint32_t x = ro & ~3u; x < re; x += 4) {
                 const uint4 q = st4[x >> 2];
                 rk += (q.x < k) + (q.y < k) + (q.z < k) + (q.w < k);
             }
+#endif
             rk += ro & ~3u;  // keys before the first read: all of earlier rows, all smaller
             const S v = Sem::finish(hvals, sl);
             if (Sem::is_zero(v)) zero(lr);
