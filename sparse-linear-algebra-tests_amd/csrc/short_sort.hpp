@@ -24,88 +24,6 @@ namespace slat {
 constexpr uint32_t kSortG = 64;     // ELL groups per batch: one per lane
 constexpr uint32_t kSortEnt = 256;  // A entries per batch: kRegQ per lane
 
-// value of lane (lane ^ M): DPP quad permutes for 1 and 2, ds_swizzle (bit-mask mode, within 32
-// lanes) up to 16, ds_bpermute for 32
-template <int M>
-__device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
-    if constexpr (M == 1)
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
-    else if constexpr (M == 2)
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
-    else if constexpr (M < 32)
-        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (M << 10) | 0x1F);
-    else
-        return (uint32_t)__shfl_xor((int)x, 32);
-}
-template <int M, typename T>
-__device__ __forceinline__ T lane_xor_t(T v) {
-    if constexpr (sizeof(T) == 4) {
-        return __builtin_bit_cast(T, lane_xor<M>(__builtin_bit_cast(uint32_t, v)));
-    } else {
-        const uint64_t u = __builtin_bit_cast(uint64_t, v);
-        return __builtin_bit_cast(T, ((uint64_t)lane_xor<M>((uint32_t)(u >> 32)) << 32) | lane_xor<M>((uint32_t)u));
-    }
-}
-
-// One compare-exchange step (K, J) of the bitonic network over 256 elements, element i = lane * 4 + e.
-// Ties keep their own payload, so the pair never duplicates or loses one.
-template <int K, int J, bool HV, typename T>
-__device__ __forceinline__ void bitonic_step(uint32_t (&k)[4], T (&v)[4], uint32_t lane) {
-    if constexpr (J >= 4) {
-        constexpr int M = J / 4;
-        const bool asc = (lane & (K / 4)) == 0;
-        const bool tmin = ((lane & M) == 0) == asc;
-        sfor<4>([&](auto E) {
-            constexpr int e = decltype(E)::value;
-            const uint32_t pk = lane_xor<M>(k[e]);
-            const bool sw = tmin ? pk < k[e] : pk > k[e];
-            if constexpr (HV) {
-                const T pv = lane_xor_t<M>(v[e]);
-                v[e] = sw ? pv : v[e];
-            }
-            k[e] = sw ? pk : k[e];
-        });
-    } else {
-        sfor<4>([&](auto E) {
-            constexpr int e = decltype(E)::value;
-            if constexpr ((e & J) == 0) {
-                constexpr int f = e | J;
-                const bool asc = (((lane << 2) | (uint32_t)e) & (uint32_t)K) == 0;
-                const bool sw = asc ? k[e] > k[f] : k[e] < k[f];
-                const uint32_t t = k[e];
-                k[e] = sw ? k[f] : t;
-                k[f] = sw ? t : k[f];
-                if constexpr (HV) {
-                    const T tv = v[e];
-                    v[e] = sw ? v[f] : tv;
-                    v[f] = sw ? tv : v[f];
-                }
-            }
-        });
-    }
-}
-template <int K, int J, bool HV, typename T>
-__device__ __forceinline__ void bitonic_merge(uint32_t (&k)[4], T (&v)[4], uint32_t lane) {
-    bitonic_step<K, J, HV, T>(k, v, lane);
-    if constexpr (J > 1) bitonic_merge<K, J / 2, HV, T>(k, v, lane);
-}
-// ascending sort of the wave's 256 keys (kSent last), payloads travel with their keys
-template <bool HV, typename T>
-__device__ __forceinline__ void wave_sort256(uint32_t (&k)[4], T (&v)[4]) {
-#ifdef SLAT_EXP_NOSORT
-    return;
-#endif
-    const uint32_t lane = (uint32_t)lane_id();
-    bitonic_merge<2, 1, HV, T>(k, v, lane);
-    bitonic_merge<4, 2, HV, T>(k, v, lane);
-    bitonic_merge<8, 4, HV, T>(k, v, lane);
-    bitonic_merge<16, 8, HV, T>(k, v, lane);
-    bitonic_merge<32, 16, HV, T>(k, v, lane);
-    bitonic_merge<64, 32, HV, T>(k, v, lane);
-    bitonic_merge<128, 64, HV, T>(k, v, lane);
-    bitonic_merge<256, 128, HV, T>(k, v, lane);
-}
-
 // key of element i + 1 (kSent past the end)
 __device__ __forceinline__ void next_keys(const uint32_t (&k)[4], uint32_t (&nk)[4]) {
     uint32_t n0 = (uint32_t)__shfl_down((int)k[0], 1);

@@ -1687,10 +1687,46 @@ static __global__ __launch_bounds__(kBlock) void k_row_bound(const uint64_t *a_r
     }
 }
 
+// Positions of the batch's (A entry, ELL group) pairs in group order: exclusive prefix of the group
+// counts over the entries (kRegQ rounds of the wave). Returns the number of groups.
+__device__ __forceinline__ uint32_t group_positions(const uint32_t (&ng)[kRegQ], uint32_t (&pos)[kRegQ]) {
+    uint32_t tot = 0;
+    sfor<kRegQ>([&](auto Q) {
+        const uint32_t incl = wave_incl_scan(ng[Q], 0u, [](uint32_t x, uint32_t y) { return x + y; });
+        pos[Q] = tot + incl - ng[Q];
+        tot += readlane_u32(incl, kWave - 1);
+    });
+    return tot;
+}
+
+// The pairs of group positions [base, base + kStageG) staged one per slot, so the accumulation
+// runs one group per lane (every lane busy) instead of one A entry per lane and group index (C4:
+// a quarter of the lanes): gk = B row | group << 24 (B rows < 2^24 with the ELL copy), gl = local
+// row, ga = A value.
+constexpr uint32_t kStageG = 256;
+template <bool VALS, typename S>
+__device__ __forceinline__ void stage_groups(uint32_t base, uint32_t mxg, const uint32_t (&kq)[kRegQ],
+                                             const uint32_t (&lq)[kRegQ], const uint32_t (&ng)[kRegQ],
+                                             const uint32_t (&pos)[kRegQ], const S (&aq)[kRegQ], uint32_t *gk,
+                                             uint8_t *gl, S *ga) {
+    for (uint32_t t = 0; t < mxg; ++t)
+        sfor<kRegQ>([&](auto Q) {
+            const uint32_t g = pos[Q] + t - base;  // wraps past kStageG below base
+            if (t < ng[Q] && g < kStageG) {
+                gk[g] = kq[Q] | (t << 24);
+                gl[g] = (uint8_t)lq[Q];
+                if constexpr (VALS) ga[g] = aq[Q];
+            }
+        });
+    wave_sync();
+}
+
 // Symbolic of the short rows of a wide launch, batched like k_numeric_short: tiles of 64 rows,
 // runs of consecutive rows with product bound <= 0.7 kSymHashT and <= 256 entries share one
 // table of composite keys; a fresh insert counts for its row. Other rows go to p.list.
-__host__ __device__ constexpr uint32_t sym_short_bytes() { return kSymHashT * 4 + 256 * 4 + kWave * 4; }
+// LDS per wave: keys u32[kSymHashT] | entry markers u32[256] | row counts u32[64] | staged groups:
+// gk u32[kStageG], gl u8[kStageG]
+__host__ __device__ constexpr uint32_t sym_short_bytes() { return kSymHashT * 4 + 256 * 4 + kWave * 4 + kStageG * 5; }
 
 template <typename I>
 __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
@@ -1700,7 +1736,8 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     uint32_t *keys = smem + (size_t)wv * (sym_short_bytes() / 4);
-    uint32_t *marks = keys + kSymHashT, *rcnt = marks + 256;
+    uint32_t *marks = keys + kSymHashT, *rcnt = marks + 256, *gk = rcnt + kWave;
+    uint8_t *gl = (uint8_t *)(gk + kStageG);
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) p.c_rp[0] = 0;
         if (threadIdx.x < kShards) {
@@ -1764,28 +1801,34 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
                 mxg = max(mxg, ng[Q]);
             });
             mxg = wave_max_u32(mxg);
-            uint32_t nprod = 0;
-            for (uint32_t t = 0; t < mxg; ++t) {
-                uint4 c[kRegQ];
-                sfor<kRegQ>([&](auto Q) {
-                    c[Q] = make_uint4(kSent, kSent, kSent, kSent);
-                    if (t < ng[Q]) c[Q] = ell_cols(p, kq[Q], t);
-                });
-                sfor<kRegQ>([&](auto Q) {
-                    const uint32_t hi = lq[Q] << cb;
-                    uint32_t cc[4] = {c[Q].x, c[Q].y, c[Q].z, c[Q].w}, sl[4];
+            uint32_t nprod = 0, pos[kRegQ];
+            const uint32_t G = group_positions(ng, pos);
+            const uint32_t noval[kRegQ] = {};
+            for (uint32_t base = 0; base < G; base += kStageG) {
+                stage_groups<false, uint32_t>(base, mxg, kq, lq, ng, pos, noval, gk, gl, nullptr);
+                const uint32_t n = min(G - base, kStageG);
+                for (uint32_t g0 = 0; g0 < n; g0 += kWave) {
+                    const uint32_t g = g0 + lane;
+                    uint32_t cc[4] = {kSent, kSent, kSent, kSent}, sl[4], lr = 0;
+                    if (g < n) {
+                        const uint32_t w = gk[g];
+                        const uint4 c = ell_cols(p, w & 0xFFFFFFu, w >> 24);
+                        lr = gl[g];
+                        const uint32_t hi = lr << cb;
+                        cc[0] = c.x != kSent ? (hi | c.x) : kSent;
+                        cc[1] = c.y != kSent ? (hi | c.y) : kSent;
+                        cc[2] = c.z != kSent ? (hi | c.z) : kSent;
+                        cc[3] = c.w != kSent ? (hi | c.w) : kSent;
+                    }
                     bool fresh[4];
 #pragma unroll
-                    for (int x = 0; x < 4; ++x) {
-                        nprod += cc[x] != kSent ? 1u : 0u;
-                        cc[x] = cc[x] != kSent ? (hi | cc[x]) : kSent;
-                    }
+                    for (int x = 0; x < 4; ++x) nprod += cc[x] != kSent ? 1u : 0u;
                     hash_batch<4>(keys, 10, cc, sl, fresh);
                     const uint32_t f = (uint32_t)fresh[0] + fresh[1] + fresh[2] + fresh[3];
-                    if (f) atomicAdd(&rcnt[lq[Q]], f);
-                });
+                    if (f) atomicAdd(&rcnt[lr], f);
+                }
+                wave_sync();
             }
-            wave_sync();
             if (p.stats) flops += wave_sum_u32(nprod);
             if (inb && (uint32_t)lane < e) {
                 p.counts[r] = rcnt[lane - b];
@@ -1801,70 +1844,148 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
         atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
 }
 
-// LDS of k_numeric_short per wave: the hash table (hash_bytes) | entry -> row markers u32[256] |
-// per-row zero counts u32[64] | row order: slot of each staged key u32[256], row offsets u32[65],
-// row fill counters u32[64]
-template <typename Sem>
-__host__ __device__ constexpr uint32_t short_bytes() {
-    return hash_bytes<Sem>() + 256 * 4 + kWave * 4 + 256 * 4 + 68 * 4 + kWave * 4;
+// ------------------------------------------------------------------------------------------------
+// Wave-wide bitonic sort of 256 (key, payload) pairs, 4 per lane (element i = lane * 4 + e): the
+// emit order of the hash categories' keys (and the sorted short-row experiment, short_sort.hpp).
+// ------------------------------------------------------------------------------------------------
+// value of lane (lane ^ M): DPP quad permutes for 1 and 2, ds_swizzle (bit-mask mode, within 32
+// lanes) up to 16, ds_bpermute for 32
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
+    if constexpr (M == 1)
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    else if constexpr (M == 2)
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    else if constexpr (M < 32)
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (M << 10) | 0x1F);
+    else
+        return (uint32_t)__shfl_xor((int)x, 32);
+}
+template <int M, typename T>
+__device__ __forceinline__ T lane_xor_t(T v) {
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, lane_xor<M>(__builtin_bit_cast(uint32_t, v)));
+    } else {
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        return __builtin_bit_cast(T, ((uint64_t)lane_xor<M>((uint32_t)(u >> 32)) << 32) | lane_xor<M>((uint32_t)u));
+    }
 }
 
-// Emit of a batch of rows held in the hash table: keys are staged grouped by row (rowoff[lr] +
-// a per-row counter), and a key's output position is rowoff[lr] + the number of keys of ITS row
-// below it (16-byte reads of the row's staged keys; composite keys of earlier rows are all
-// smaller, later rows' all larger, so reads may overrun the row's bounds). Keys are composite
-// (lr << cb | column) when cb > 0. The table, the counters are left clean; zero values go to
-// zero(local row).
+// One compare-exchange step (K, J) of the bitonic network over 256 elements, element i = lane * 4 + e.
+// Ties keep their own payload, so the pair never duplicates or loses one.
+template <int K, int J, bool HV, typename T>
+__device__ __forceinline__ void bitonic_step(uint32_t (&k)[4], T (&v)[4], uint32_t lane) {
+    if constexpr (J >= 4) {
+        constexpr int M = J / 4;
+        const bool asc = (lane & (K / 4)) == 0;
+        const bool tmin = ((lane & M) == 0) == asc;
+        sfor<4>([&](auto E) {
+            constexpr int e = decltype(E)::value;
+            const uint32_t pk = lane_xor<M>(k[e]);
+            const bool sw = tmin ? pk < k[e] : pk > k[e];
+            if constexpr (HV) {
+                const T pv = lane_xor_t<M>(v[e]);
+                v[e] = sw ? pv : v[e];
+            }
+            k[e] = sw ? pk : k[e];
+        });
+    } else {
+        sfor<4>([&](auto E) {
+            constexpr int e = decltype(E)::value;
+            if constexpr ((e & J) == 0) {
+                constexpr int f = e | J;
+                const bool asc = (((lane << 2) | (uint32_t)e) & (uint32_t)K) == 0;
+                const bool sw = asc ? k[e] > k[f] : k[e] < k[f];
+                const uint32_t t = k[e];
+                k[e] = sw ? k[f] : t;
+                k[f] = sw ? t : k[f];
+                if constexpr (HV) {
+                    const T tv = v[e];
+                    v[e] = sw ? v[f] : tv;
+                    v[f] = sw ? tv : v[f];
+                }
+            }
+        });
+    }
+}
+template <int K, int J, bool HV, typename T>
+__device__ __forceinline__ void bitonic_merge(uint32_t (&k)[4], T (&v)[4], uint32_t lane) {
+    bitonic_step<K, J, HV, T>(k, v, lane);
+    if constexpr (J > 1) bitonic_merge<K, J / 2, HV, T>(k, v, lane);
+}
+// ascending sort of the wave's 256 keys (kSent last), payloads travel with their keys
+template <bool HV, typename T>
+__device__ __forceinline__ void wave_sort256(uint32_t (&k)[4], T (&v)[4]) {
+    const uint32_t lane = (uint32_t)lane_id();
+    bitonic_merge<2, 1, HV, T>(k, v, lane);
+    bitonic_merge<4, 2, HV, T>(k, v, lane);
+    bitonic_merge<8, 4, HV, T>(k, v, lane);
+    bitonic_merge<16, 8, HV, T>(k, v, lane);
+    bitonic_merge<32, 16, HV, T>(k, v, lane);
+    bitonic_merge<64, 32, HV, T>(k, v, lane);
+    bitonic_merge<128, 64, HV, T>(k, v, lane);
+    bitonic_merge<256, 128, HV, T>(k, v, lane);
+}
+
+// LDS of k_numeric_short per wave: the hash table (hash_bytes: keys | values | staged keys u32[260])
+// | entry -> row markers u32[256] | per-row zero counts u32[64] | slots of the staged keys u32[256]
+// (staging of the accumulation: gk in the staged-key words, ga S[256] over the markers onward, which
+// are cleared after it) | gl u8[kStageG]
+template <typename Sem>
+__host__ __device__ constexpr uint32_t short_bytes() {
+    return hash_bytes<Sem>() + 256 * 4 + kWave * 4 + 256 * 4 + kStageG;
+}
+
+// Emit of a batch of rows held in the hash table (<= 256 keys, all distinct): the keys and their
+// slots are compacted into hstage / hslot, loaded 4 per lane and sorted across the wave
+// (wave_sort256); a key's sorted position IS its output index in the batch, since keys are
+// composite (lr << cb | column, cb > 0) and the batch's rows are contiguous in C. The table is left
+// clean; zero values go to zero(local row).
 template <typename Sem, typename Z>
 __device__ __forceinline__ void batch_emit(uint32_t *hkeys, typename Sem::V *hvals, uint32_t *hstage, uint32_t *hslot,
-                                           const uint32_t *rowoff, uint32_t *rowctr, uint32_t cb, uint32_t tot,
-                                           uint32_t *oc, typename Sem::S *ov, Z &&zero) {
+                                           uint32_t cb, uint32_t tot, uint32_t *oc, typename Sem::S *ov, Z &&zero) {
     using S = typename Sem::S;
     using V = typename Sem::V;
-    const int lane = lane_id();
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t hk[kHashHeld], nh = 0;
     sfor<kHashHeld>([&](auto I_) {
-        const uint32_t sl = I_ * kWave + lane;
-        const uint32_t k = hkeys[sl];
-        if (k != kSent) {
-            const uint32_t lr = cb ? k >> cb : 0u;
-            const uint32_t pos = rowoff[lr] + atomicAdd(&rowctr[lr], 1u);
-            if (pos < tot) {
-                hstage[pos] = k;
-                hslot[pos] = sl;
+        hk[I_] = hkeys[I_ * kWave + lane];
+        nh += hk[I_] != kSent ? 1u : 0u;
+    });
+    const uint32_t incl = wave_incl_scan(nh, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    const uint32_t nk = min(readlane_u32(incl, kWave - 1), kHashT / 2);
+    uint32_t at = incl - nh;
+    sfor<kHashHeld>([&](auto I_) {
+        if (hk[I_] != kSent) {
+            if (at < kHashT / 2) {
+                hstage[at] = hk[I_];
+                hslot[at] = I_ * kWave + lane;
             }
-            hkeys[sl] = kSent;
+            ++at;
+            hkeys[I_ * kWave + lane] = kSent;
         }
     });
-    if (lane < 4) hstage[tot + lane] = kSent;  // pad for the 16-byte reads
     wave_sync();
+    const uint4 k4 = ((const uint4 *)hstage)[lane], s4 = ((const uint4 *)hslot)[lane];
+    uint32_t k[4] = {k4.x, k4.y, k4.z, k4.w}, sl[4] = {s4.x, s4.y, s4.z, s4.w};
+    sfor<4>([&](auto E) {
+        if (lane * 4 + E >= nk) k[E] = kSent;
+    });
+    wave_sort256<true, uint32_t>(k, sl);
     const uint32_t cmask = cb ? (1u << cb) - 1 : 0xFFFFFFFFu;
-    const uint4 *st4 = (const uint4 *)hstage;
-#pragma unroll
-    for (int m = 0; m < (int)(kHashT / 2 / kWave); ++m) {
-        const uint32_t j = m * kWave + lane;
-        if (j < tot) {
-            const uint32_t k = hstage[j], sl = hslot[j];
-            const uint32_t lr = cb ? k >> cb : 0u;
-            const uint32_t ro = rowoff[lr], re = rowoff[lr + 1];
-            uint32_t rk = 0;
-#ifndef SLAT_EXP_NORANK
-            for (uint32_t x = ro & ~3u; x < re; x += 4) {
-                const uint4 q = st4[x >> 2];
-                rk += (q.x < k) + (q.y < k) + (q.z < k) + (q.w < k);
-            }
-#endif
-            rk += ro & ~3u;  // keys before the first read: all of earlier rows, all smaller
-            const S v = Sem::finish(hvals, sl);
-            if (Sem::is_zero(v)) zero(lr);
-            if (rk < tot) {
-                oc[rk] = k & cmask;
-                ov[rk] = v;
+    sfor<4>([&](auto E) {
+        const uint32_t i = lane * 4 + E;
+        if (k[E] != kSent) {
+            const S v = Sem::finish(hvals, sl[E]);
+            if (Sem::is_zero(v)) zero(cb ? k[E] >> cb : 0u);
+            if (i < tot) {  // never write past the batch's slice
+                oc[i] = k[E] & cmask;
+                ov[i] = v;
             }
 #pragma unroll
-            for (int w = 0; w < Sem::kSlots; ++w) hvals[sl * Sem::kSlots + w] = V(0);
+            for (int w = 0; w < Sem::kSlots; ++w) hvals[sl[E] * Sem::kSlots + w] = V(0);
         }
-    }
-    if (lane < 64) rowctr[lane] = 0;
+    });
     wave_sync();
 }
 
@@ -1883,12 +2004,15 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
     uint32_t *hstage = (uint32_t *)(region + kHashT * 4 + kHashT * sizeof(V) * Sem::kSlots);
     uint32_t *marks = (uint32_t *)(region + hash_bytes<Sem>());
     uint32_t *zc = marks + 256;
-    uint32_t *hslot = zc + kWave, *rowoff = hslot + 256, *rowctr = rowoff + 68;
+    uint32_t *hslot = zc + kWave;
+    uint32_t *gk = hstage;
+    S *ga = (S *)marks;  // 256 * sizeof(S) <= markers + zero counts + slots
+    uint8_t *gl = (uint8_t *)(hslot + 256);
+    static_assert(kStageG * sizeof(S) <= (256 + kWave + 256) * 4, "staged A values overrun");
     for (uint32_t w = lane; w < kHashT; w += kWave) hkeys[w] = kSent;
     for (uint32_t w = lane; w < kHashT * Sem::kSlots; w += kWave) hvals[w] = V(0);
     for (uint32_t w = lane; w < 256; w += kWave) marks[w] = 0;
     zc[lane] = 0;
-    rowctr[lane] = 0;
     wave_sync();
     // pattern B (every B value equal): no B-value loads (u32 with the ELL copy, as k_numeric)
     uint32_t bvmax = 0;
@@ -1908,6 +2032,8 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
     uint32_t zrows = 0;
     const uint32_t cb = p.cbits;
     const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
+    PhaseClock pc{};  // diagnostic builds (SLAT_PHASES): where the waves' time goes
+    if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
     for (uint64_t tile = (uint64_t)blockIdx.x * kWpb + wv; tile < ntiles; tile += (uint64_t)gridDim.x * kWpb) {
         const uint64_t r0 = tile * kWave, r = r0 + lane;
         const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
@@ -1937,6 +2063,8 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
             const unsigned long long stop = __ballot(inb && (!shortj || pu > kHashT / 2 || pl > 256 ||
                                                              (cb == 0 && (uint32_t)lane > b)));
             const uint32_t e = stop ? (uint32_t)__builtin_ctzll(stop) : nt;
+            pc.mark(0);  // tile header, batch formation
+            pc.ph[kPhaseSlots - 1] += 1;
             const uint64_t A0 = readlane_u64(A0j, (int)b);
             const uint64_t OB = readlane_u64(obj, (int)b);
             HashAcc<Sem> ha{hkeys, hvals};
@@ -1947,12 +2075,8 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
                 lim = (uint32_t)readlane_u64(uj, (int)b);
                 RowWalker<Sem, I, true, true> rw(p, (I)A0, (I)A1);
                 rw.template each_group<true>(ha);
-                if (lane == 0) {
-                    rowoff[0] = 0;
-                    rowoff[1] = lim;
-                }
                 wave_sync();
-                batch_emit<Sem>(hkeys, hvals, hstage, hslot, rowoff, rowctr, 0u, lim, p.c_col + OB, cval + OB,
+                batch_emit<Sem>(hkeys, hvals, hstage, hslot, 0u, lim, p.c_col + OB, cval + OB,
                                 [&](uint32_t) { atomicAdd(&zc[0], 1u); });
                 if ((uint32_t)lane == b) {
                     const uint32_t z = zc[0];
@@ -1994,34 +2118,38 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
                 mxg = max(mxg, ng[Q]);
             });
             mxg = wave_max_u32(mxg);
-            for (uint32_t t = 0; t < mxg; ++t) {
-                uint4 c[kRegQ];
-                Quad<S> pv[kRegQ];
-                sfor<kRegQ>([&](auto Q) {
-                    c[Q] = make_uint4(kSent, kSent, kSent, kSent);
-                    pv[Q] = Quad<S>{};
-                    if (t < ng[Q]) {
-                        c[Q] = ell_cols(p, kq[Q], t);
-                        if (!buni) pv[Q] = ell_vals<S>(p, kq[Q], t);
+            pc.mark(1);  // A entries, local rows, group counts
+            uint32_t pos[kRegQ];
+            const uint32_t G = group_positions(ng, pos);
+            for (uint32_t base = 0; base < G; base += kStageG) {
+                stage_groups<true, S>(base, mxg, kq, lq, ng, pos, aq, gk, gl, ga);
+                const uint32_t n = min(G - base, kStageG);
+                for (uint32_t g0 = 0; g0 < n; g0 += kWave) {
+                    const uint32_t g = g0 + lane;
+                    uint4 ck = make_uint4(kSent, kSent, kSent, kSent);
+                    Quad<S> pr{};
+                    if (g < n) {
+                        const uint32_t w = gk[g], bk = w & 0xFFFFFFu, t = w >> 24;
+                        const uint4 c = ell_cols(p, bk, t);
+                        const S a = ga[g];
+                        pr = buni ? splat4(Sem::prod(a, bv0)) : prods<Sem>(a, ell_vals<S>(p, bk, t));
+                        const uint32_t hi = (uint32_t)gl[g] << cb;
+                        ck.x = c.x != kSent ? (hi | c.x) : kSent;
+                        ck.y = c.y != kSent ? (hi | c.y) : kSent;
+                        ck.z = c.z != kSent ? (hi | c.z) : kSent;
+                        ck.w = c.w != kSent ? (hi | c.w) : kSent;
                     }
-                });
-                sfor<kRegQ>([&](auto Q) {
-                    const Quad<S> pr = buni ? splat4(Sem::prod(aq[Q], bv0)) : prods<Sem>(aq[Q], pv[Q]);
-                    const uint32_t hi = lq[Q] << cb;
-                    uint4 ck = c[Q];
-                    ck.x = ck.x != kSent ? (hi | ck.x) : kSent;
-                    ck.y = ck.y != kSent ? (hi | ck.y) : kSent;
-                    ck.z = ck.z != kSent ? (hi | ck.z) : kSent;
-                    ck.w = ck.w != kSent ? (hi | ck.w) : kSent;
                     ha(ck, pr);
-                });
+                }
+                wave_sync();
             }
-            // row offsets within the batch: exclusive prefix of the output counts
-            if (inb && (uint32_t)lane < e) rowoff[lane - b] = pu - uu;
-            if ((uint32_t)lane == e - 1) rowoff[e - b] = pu;
+            // the staged A values overwrote the entry markers and zero counts: clear them
+            for (uint32_t w = lane; w < kStageG * sizeof(S) / 16; w += kWave) ((uint4 *)marks)[w] = make_uint4(0, 0, 0, 0);
             wave_sync();
-            batch_emit<Sem>(hkeys, hvals, hstage, hslot, rowoff, rowctr, cb, lim, p.c_col + OB, cval + OB,
+            pc.mark(2);  // ELL loads, hash accumulation
+            batch_emit<Sem>(hkeys, hvals, hstage, hslot, cb, lim, p.c_col + OB, cval + OB,
                             [&](uint32_t lr) { atomicAdd(&zc[lr], 1u); });
+            pc.mark(3);  // emit
             if (inb && (uint32_t)lane < e) {
                 const uint32_t z = zc[lane - b];
                 p.counts[r] = uj - z;
@@ -2030,7 +2158,14 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
             wave_sync();
             if (inb && (uint32_t)lane < e) zc[lane - b] = 0;
             wave_sync();
+            pc.mark(4);  // counts
             b = e;
+        }
+    }
+    if constexpr (SLAT_PHASES) {
+        if (lane == 0) {
+            unsigned long long *dst = p.shards + 512 + ((blockIdx.x * kWpb + wv) % 64) * kPhaseSlots;
+            for (int i = 0; i < kPhaseSlots; ++i) atomicAdd(&dst[i], (unsigned long long)pc.ph[i]);
         }
     }
     zrows = wave_sum_u32(zrows);
