@@ -15,7 +15,7 @@
 //
 // Per row the batch formation needs the row's ELL group count: the symbolic kernel computes it
 // from the tile's entries (coalesced a_col loads, a wave prefix of the group counts read at each
-// row's ends) and stores it for the numeric kernel, replacing k_row_bound.
+// row's ends, as k_symbolic_short's tile_groups) and stores it for the numeric kernel.
 #pragma once
 #include "spgemm_kernels.hpp"
 

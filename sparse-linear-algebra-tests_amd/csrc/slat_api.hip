@@ -406,7 +406,12 @@ static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hi
         return hipGetLastError();
     }
     if (a.hash == 3) {  // batched short rows (integer semirings, ELL B)
-        if constexpr (!Sem::kOrdered) {
+        if constexpr (std::is_same_v<Sem, SemU32>) {
+            if (idx32)
+                hipLaunchKernelGGL((k_numeric_short_u32<uint32_t>), grid, dim3(kBlock), lds, s, a);
+            else
+                hipLaunchKernelGGL((k_numeric_short_u32<uint64_t>), grid, dim3(kBlock), lds, s, a);
+        } else if constexpr (!Sem::kOrdered) {
             if (idx32)
                 hipLaunchKernelGGL((k_numeric_short<Sem, uint32_t>), grid, dim3(kBlock), lds, s, a);
             else
@@ -465,7 +470,9 @@ static int numeric_blocks_per_cu(bool idx32, bool ell, int mode, size_t lds) {
         else
             e = hipErrorInvalidValue;
     } else if (mode == 3) {
-        if constexpr (!Sem::kOrdered)
+        if constexpr (std::is_same_v<Sem, SemU32>)
+            e = idx32 ? occ(k_numeric_short_u32<uint32_t>) : occ(k_numeric_short_u32<uint64_t>);
+        else if constexpr (!Sem::kOrdered)
             e = idx32 ? occ(k_numeric_short<Sem, uint32_t>) : occ(k_numeric_short<Sem, uint64_t>);
         else
             e = hipErrorInvalidValue;
@@ -683,7 +690,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const bool batched = sym_batched && (dt != SLAT_F64 || f64any);
     // experiment (SLAT_SORT_SHORT=1): the batched short rows sorted in registers (short_sort.hpp)
     // instead of LDS hash tables. Measured on C4 (100^3, A^3 * A): symbolic 1.06 ms vs 0.52 ms
-    // (k_row_bound + k_symbolic_short), numeric 1.58 + 0.41 ms (rows past 64 groups in the window
+    // (the row-bound kernel + k_symbolic_short at the time), numeric 1.58 + 0.41 ms (rows past 64 groups in the window
     // launch) vs 1.47 ms: one sort of 256 slots serves ~2 C4 rows against ~4-8 rows per hash
     // table, so the hash category stays the default
     static const bool kSortShort = std::getenv("SLAT_SORT_SHORT") != nullptr;
@@ -841,16 +848,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
     if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return st;
     if (sym_batched) {
-        // MAGNUS categorisation: product bound per row, then the short rows batched in hash tables
-        // (listing the rest), then the listed rows by windows
+        // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
+        // row's products per tile, listing the rest), then the listed rows by windows
         unsigned int *lc = (unsigned int *)(ws + o_lc);
         SLAT_HIP(ctx, hipMemsetAsync(lc, 0, lc_b, s));
         uint32_t *rb = (uint32_t *)(ws + o_rb);
-        if (!sorted)
-            hipLaunchKernelGGL(k_row_bound,
-                               dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kBlock - 1) / kBlock, ctx->cu_count * 8ull))),
-                               dim3(kBlock), 0, s, a.a_rp, a.a_col, n, a.b_nrows, a.ell_ng, rb);
-        SLAT_HIP(ctx, hipGetLastError());
         Args h1 = asym, h2 = asym;
         h1.rbound = rb;
         h1.cbits = a.cbits;

@@ -99,7 +99,7 @@ struct Args {
     uint32_t hash;
     uint32_t b_maxrow;
     uint32_t cbits;     // k_*_short: column bits of the composite (row, column) keys (0: one row per batch)
-    const uint32_t *rbound;  // k_symbolic_short: product bound per row (k_row_bound)
+    const uint32_t *rbound;  // experiment (short_sort.hpp): ELL groups per row, written by k_symbolic_sort
     // rows of the window category, appended by the short-row kernels (symbolic / numeric lists)
     // and walked by the MODE 2 launches instead of every row
     uint32_t *list;
@@ -591,6 +591,35 @@ constexpr uint32_t kHashT = 512;      // numeric slots per wave (rows with <= kH
 constexpr uint32_t kSymHashT = 1024;  // symbolic keys per wave (rows with <= 0.7 * kSymHashT products)
 constexpr uint32_t kHashHeld = kHashT / kWave;
 
+// u32 short rows (k_numeric_short): u32 slots plus one wrap bit per slot after them instead of u64
+// slots; all terms are non-negative, so a wrap happens iff the exact sum reaches 2^32 and the
+// Saturating<u32> sum is then u32::MAX (src/graph_csr.rs:29-37). 2 KB less LDS per wave.
+struct SemU32W {
+    using S = uint32_t;
+    using P = uint32_t;
+    using V = uint32_t;
+    static constexpr int kSlots = 1;
+    static constexpr bool kOrdered = false;
+    static constexpr bool kNarrowable = true;
+    static constexpr uint32_t kExtraWords = kHashT / 32;  // the wrap bits
+    __device__ static __forceinline__ P prod(S a, S b) { return SemU32::prod(a, b); }
+    __device__ static __forceinline__ void acc(V *vals, uint32_t r, P p) {
+        const uint32_t old = atomicAdd(&vals[r], p);
+        if (old + p < old) atomicOr(&vals[kHashT + (r >> 5)], 1u << (r & 31));
+    }
+    __device__ static __forceinline__ S finish(const V *vals, uint32_t t) {
+        return (vals[kHashT + (t >> 5)] >> (t & 31)) & 1u ? 0xFFFFFFFFu : vals[t];
+    }
+    __device__ static __forceinline__ bool is_zero(S v) { return v == 0; }
+};
+template <typename Sem, typename = void>
+struct ExtraWords : std::integral_constant<uint32_t, 0> {};
+template <typename Sem>
+struct ExtraWords<Sem, std::void_t<decltype(Sem::kExtraWords)>> : std::integral_constant<uint32_t, Sem::kExtraWords> {};
+// the semiring k_numeric_short accumulates in
+template <typename Sem>
+using ShortSem = std::conditional_t<std::is_same_v<Sem, SemU32>, SemU32W, Sem>;
+
 __device__ __forceinline__ uint32_t hash_slot(uint32_t c, uint32_t logt) { return (c * 0x9E3779B1u) >> (32 - logt); }
 
 // slots of N columns at once (kSent = no column): every probe round issues all pending CAS
@@ -693,7 +722,8 @@ struct HashAcc {
 // u32[kHashT / 2 + 4] (the row's keys, compacted, padded with kSent for 16-byte reads)
 template <typename Sem>
 __host__ __device__ constexpr uint32_t hash_bytes() {
-    return kHashT * 4 + kHashT * (uint32_t)sizeof(typename Sem::V) * Sem::kSlots + (kHashT / 2 + 4) * 4;
+    return kHashT * 4 + kHashT * (uint32_t)sizeof(typename Sem::V) * Sem::kSlots + ExtraWords<Sem>::value * 4 +
+           (kHashT / 2 + 4) * 4;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1668,24 +1698,6 @@ __device__ __forceinline__ void list_rows(const Args &p, bool take, uint64_t r) 
     if (take) p.list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)r;
 }
 
-// MAGNUS row categorisation input: an upper bound of the scalar products of every row of A*B,
-// 4 x the ELL groups of the B rows it references (one lane per row; group counts sit in L2)
-static __global__ __launch_bounds__(kBlock) void k_row_bound(const uint64_t *a_rp, const uint32_t *a_col, uint64_t nrows,
-                                                      uint64_t b_nrows, const uint8_t *ell_ng, uint32_t *bound) {
-    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < nrows; r += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t a0 = a_rp[r], a1 = a_rp[r + 1];
-        uint64_t g = 0;
-        for (uint64_t i = a0; i < a1; i += 8) {  // 8 independent loads per round
-            uint32_t k[8];
-#pragma unroll
-            for (int x = 0; x < 8; ++x) k[x] = i + x < a1 ? a_col[i + x] : 0xFFFFFFFFu;
-#pragma unroll
-            for (int x = 0; x < 8; ++x)
-                if (k[x] < b_nrows) g += ell_ng[k[x]];
-        }
-        bound[r] = (uint32_t)min<uint64_t>(4 * g, 0xFFFFFFFFull);
-    }
-}
 
 // Positions of the batch's (A entry, ELL group) pairs in group order: exclusive prefix of the group
 // counts over the entries (kRegQ rounds of the wave). Returns the number of groups.
@@ -1719,6 +1731,46 @@ __device__ __forceinline__ void stage_groups(uint32_t base, uint32_t mxg, const 
             }
         });
     wave_sync();
+}
+
+// MAGNUS row categorisation input: the ELL groups of each row of a 64-row tile (lane j: row r0 + j),
+// i.e. a product bound of 4 per group, from the tile's entries with coalesced loads: the exclusive
+// prefix of the entries' group counts, read at each row's first and end entry (mod 2^32: only rows
+// of <= 256 entries use the difference, and the entries of longer rows are skipped, not read).
+// pf: u32[256] of LDS, left dirty.
+__device__ __forceinline__ uint32_t tile_groups(const Args &p, uint64_t A0j, uint64_t A1j, uint32_t nt, uint32_t *pf) {
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint64_t T0 = readlane_u64(A0j, 0), T1 = readlane_u64(A1j, (int)nt - 1);
+    const bool longj = lane < nt && A1j - A0j > 256;
+    uint32_t gs = 0, ge = 0, run = 0;
+    for (uint64_t c0 = T0; c0 < T1;) {
+        const unsigned long long in = __ballot(longj && A0j <= c0 && c0 < A1j);
+        if (in) {  // inside a long row: jump to its end
+            if (A0j == c0) gs = run;
+            if (A1j == c0) ge = run;
+            c0 = readlane_u64(A1j, (int)__builtin_ctzll(in));
+            continue;
+        }
+        uint32_t kk[4], g[4];
+        sfor<4>([&](auto Q) {
+            const uint64_t idx = c0 + Q * kWave + lane;
+            kk[Q] = idx < T1 ? p.a_col[idx] : kSent;
+        });
+        sfor<4>([&](auto Q) { g[Q] = kk[Q] < p.b_nrows ? (uint32_t)p.ell_ng[kk[Q]] : 0u; });
+        sfor<4>([&](auto Q) {
+            const uint32_t incl = wave_incl_scan(g[Q], 0u, [](uint32_t x, uint32_t y) { return x + y; });
+            pf[Q * kWave + lane] = run + incl - g[Q];
+            run += readlane_u32(incl, kWave - 1);
+        });
+        wave_sync();
+        if (A0j >= c0 && A0j < T1 && A0j - c0 < 256) gs = pf[A0j - c0];
+        if (A1j >= c0 && A1j < T1 && A1j - c0 < 256) ge = pf[A1j - c0];
+        wave_sync();
+        c0 += 256;
+    }
+    if (A0j >= T1) gs = run;
+    if (A1j >= T1) ge = run;
+    return lane < nt ? ge - gs : 0u;
 }
 
 // Symbolic of the short rows of a wide launch, batched like k_numeric_short: tiles of 64 rows,
@@ -1756,13 +1808,16 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
         const uint64_t r0 = tile * kWave, r = r0 + lane;
         const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
         uint64_t A0j = 0, A1j = 0;
-        uint32_t bj = 0;
         if ((uint32_t)lane < nt) {
             A0j = p.a_rp[r];
             A1j = p.a_rp[r + 1];
-            bj = p.rbound[r];
         }
         const uint64_t lj = A1j - A0j;
+        // product bound: 4 per ELL group (the markers serve as the prefix window, then are cleared)
+        const uint32_t gj = tile_groups(p, A0j, A1j, nt, marks);
+        const uint32_t bj = gj > 0x3FFFFFFFu ? 0xFFFFFFFFu : 4 * gj;
+        ((uint4 *)marks)[lane] = make_uint4(0, 0, 0, 0);
+        wave_sync();
         const bool fatj = (uint32_t)lane < nt && fat_row(p, r);
         const bool shortj = (uint32_t)lane < nt && bj <= kCap && lj <= 256 && !fatj;
         const unsigned long long shortm = __ballot(shortj);
@@ -1927,13 +1982,17 @@ __device__ __forceinline__ void wave_sort256(uint32_t (&k)[4], T (&v)[4]) {
     bitonic_merge<256, 128, HV, T>(k, v, lane);
 }
 
-// LDS of k_numeric_short per wave: the hash table (hash_bytes: keys | values | staged keys u32[260])
-// | entry -> row markers u32[256] | per-row zero counts u32[64] | slots of the staged keys u32[256]
-// (staging of the accumulation: gk in the staged-key words, ga S[256] over the markers onward, which
-// are cleared after it) | gl u8[kStageG]
+// LDS of k_numeric_short per wave: the hash table of ShortSem<Sem> (hash_bytes: keys | values |
+// staged keys u32[260], which also stage the groups' B rows gk) | scratch of short_mx bytes, in turn
+// the entry -> row markers u32[256], the staged A values ga S[256] and the emit's slots u32[256]
+// (cleared after each batch) | per-row zero counts u32[64] | staged local rows gl u8[kStageG]
+template <typename Sem>
+__host__ __device__ constexpr uint32_t short_mx() {
+    return 256 * (uint32_t)sizeof(typename Sem::S) > 1024 ? 256 * (uint32_t)sizeof(typename Sem::S) : 1024;
+}
 template <typename Sem>
 __host__ __device__ constexpr uint32_t short_bytes() {
-    return hash_bytes<Sem>() + 256 * 4 + kWave * 4 + 256 * 4 + kStageG;
+    return hash_bytes<ShortSem<Sem>>() + short_mx<Sem>() + kWave * 4 + kStageG;
 }
 
 // Emit of a batch of rows held in the hash table (<= 256 keys, all distinct): the keys and their
@@ -1986,11 +2045,13 @@ __device__ __forceinline__ void batch_emit(uint32_t *hkeys, typename Sem::V *hva
             for (int w = 0; w < Sem::kSlots; ++w) hvals[sl[E] * Sem::kSlots + w] = V(0);
         }
     });
+    if (lane < ExtraWords<Sem>::value) hvals[kHashT * Sem::kSlots + lane] = V(0);
     wave_sync();
 }
 
-template <typename Sem, typename I>
-__global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
+template <typename Sem0, typename I>
+__device__ __forceinline__ void numeric_short_body(Args p) {
+    using Sem = ShortSem<Sem0>;
     using S = typename Sem::S;
     using V = typename Sem::V;
     static_assert(!Sem::kOrdered, "f64 keeps the ordered single-row path");
@@ -1998,20 +2059,21 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    uint8_t *region = smem8 + (size_t)wv * short_bytes<Sem>();
+    constexpr uint32_t kMx = short_mx<Sem0>();
+    uint8_t *region = smem8 + (size_t)wv * short_bytes<Sem0>();
     uint32_t *hkeys = (uint32_t *)region;
     V *hvals = (V *)(region + kHashT * 4);
-    uint32_t *hstage = (uint32_t *)(region + kHashT * 4 + kHashT * sizeof(V) * Sem::kSlots);
+    uint32_t *hstage = (uint32_t *)(region + kHashT * 4 + kHashT * sizeof(V) * Sem::kSlots + ExtraWords<Sem>::value * 4);
     uint32_t *marks = (uint32_t *)(region + hash_bytes<Sem>());
-    uint32_t *zc = marks + 256;
-    uint32_t *hslot = zc + kWave;
+    uint32_t *hslot = marks;                // the emit's slots
+    S *ga = (S *)marks;                     // the accumulation's A values
+    uint32_t *zc = marks + kMx / 4;
     uint32_t *gk = hstage;
-    S *ga = (S *)marks;  // 256 * sizeof(S) <= markers + zero counts + slots
-    uint8_t *gl = (uint8_t *)(hslot + 256);
-    static_assert(kStageG * sizeof(S) <= (256 + kWave + 256) * 4, "staged A values overrun");
+    uint8_t *gl = (uint8_t *)(zc + kWave);
+    static_assert(kStageG * sizeof(S) <= kMx && kMx >= 1024, "scratch too small");
     for (uint32_t w = lane; w < kHashT; w += kWave) hkeys[w] = kSent;
-    for (uint32_t w = lane; w < kHashT * Sem::kSlots; w += kWave) hvals[w] = V(0);
-    for (uint32_t w = lane; w < 256; w += kWave) marks[w] = 0;
+    for (uint32_t w = lane; w < kHashT * Sem::kSlots + ExtraWords<Sem>::value; w += kWave) hvals[w] = V(0);
+    for (uint32_t w = lane; w < kMx / 16; w += kWave) ((uint4 *)marks)[w] = make_uint4(0, 0, 0, 0);
     zc[lane] = 0;
     wave_sync();
     // pattern B (every B value equal): no B-value loads (u32 with the ELL copy, as k_numeric)
@@ -2046,7 +2108,8 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
         }
         const uint64_t uj = oej - obj, lj = A1j - A0j;
         const bool fatj = (uint32_t)lane < nt && fat_row(p, r);
-        const bool shortj = (uint32_t)lane < nt && uj <= kHashT / 2 && !fatj;
+        // rows of <= 256 outputs and <= 256 A entries (rows with more entries go to the window launch)
+        const bool shortj = (uint32_t)lane < nt && uj <= kHashT / 2 && lj <= 256 && !fatj;
         const unsigned long long shortm = __ballot(shortj);
         list_rows(p, (uint32_t)lane < nt && !shortj && !fatj, r);  // the window launch's rows
         uint32_t b = 0;
@@ -2068,29 +2131,9 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
             const uint64_t A0 = readlane_u64(A0j, (int)b);
             const uint64_t OB = readlane_u64(obj, (int)b);
             HashAcc<Sem> ha{hkeys, hvals};
-            uint32_t lim;
-            if (e == b) {
-                // one short row with more than 256 entries: the walker, one segment at a time
-                const uint64_t A1 = readlane_u64(A1j, (int)b);
-                lim = (uint32_t)readlane_u64(uj, (int)b);
-                RowWalker<Sem, I, true, true> rw(p, (I)A0, (I)A1);
-                rw.template each_group<true>(ha);
-                wave_sync();
-                batch_emit<Sem>(hkeys, hvals, hstage, hslot, 0u, lim, p.c_col + OB, cval + OB,
-                                [&](uint32_t) { atomicAdd(&zc[0], 1u); });
-                if ((uint32_t)lane == b) {
-                    const uint32_t z = zc[0];
-                    p.counts[r] = uj - z;
-                    zrows += z ? 1u : 0u;
-                    zc[0] = 0;
-                }
-                ++b;
-                wave_sync();
-                continue;
-            }
             const uint64_t A1 = readlane_u64(A1j, (int)(e - 1));
             const uint32_t nent = (uint32_t)(A1 - A0);
-            lim = readlane_u32(pu, (int)(e - 1));
+            const uint32_t lim = readlane_u32(pu, (int)(e - 1));
             // entry -> local row: mark each row's first entry (a later, non-empty row wins a tie
             // with empty rows before it), then a running max over the entries
             if (inb && (uint32_t)lane < e && lj > 0) atomicMax(&marks[(uint32_t)(A0j - A0)], (uint32_t)lane - b + 1);
@@ -2143,8 +2186,6 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
                 }
                 wave_sync();
             }
-            // the staged A values overwrote the entry markers and zero counts: clear them
-            for (uint32_t w = lane; w < kStageG * sizeof(S) / 16; w += kWave) ((uint4 *)marks)[w] = make_uint4(0, 0, 0, 0);
             wave_sync();
             pc.mark(2);  // ELL loads, hash accumulation
             batch_emit<Sem>(hkeys, hvals, hstage, hslot, cb, lim, p.c_col + OB, cval + OB,
@@ -2157,6 +2198,7 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
             }
             wave_sync();
             if (inb && (uint32_t)lane < e) zc[lane - b] = 0;
+            for (uint32_t w = lane; w < kMx / 16; w += kWave) ((uint4 *)marks)[w] = make_uint4(0, 0, 0, 0);  // markers
             wave_sync();
             pc.mark(4);  // counts
             b = e;
@@ -2171,6 +2213,21 @@ __global__ __launch_bounds__(kBlock) void k_numeric_short(Args p) {
     zrows = wave_sum_u32(zrows);
     if (lane == 0 && zrows)
         __hip_atomic_fetch_add(&p.host_out[2], (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename Sem0, typename I>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_numeric_short(Args p) {
+    numeric_short_body<Sem0, I>(p);
+}
+// u32: 6 waves per SIMD (6.6 KB of LDS per wave, <= 80 VGPRs; the wider semirings are held to 4
+// waves by their LDS anyway)
+template <typename I>
+__global__ __launch_bounds__(kBlock)
+#ifndef SLAT_EXP_SHORT_W4
+__attribute__((amdgpu_waves_per_eu(6)))
+#endif
+void k_numeric_short_u32(Args p) {
+    numeric_short_body<SemU32, I>(p);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1,4 +1,5 @@
-"""The short-row category of wide launches sorted in registers (csrc/short_sort.hpp: a batch of
+"""The short-row categories of wide launches: the batched LDS hash tables (default) and the opt-in
+register sort (SLAT_SORT_SHORT=1, csrc/short_sort.hpp: a batch of
 consecutive rows with <= 64 ELL groups and <= 256 A entries, one group per lane, a bitonic sort
 over the wave, run sums by a segmented scan). Bit-exact against the oracle for u32 / Sat64, and
 within C5's stated tolerance (rtol 1e-12) for f64 in any order. Cases at the category's edges:
@@ -167,3 +168,19 @@ def test_one_row_per_batch_past_2_25_columns(dtype):
     np.testing.assert_array_equal(got.row_ptr, Cm.indptr)
     np.testing.assert_array_equal(got.col_idx, Cm.indices)
     np.testing.assert_array_equal(got.values.astype(np.float64), Cm.data)  # small integers: exact in f64
+
+
+def test_row_bounds_with_long_rows_at_chunk_edges():
+    """k_symbolic_short bounds each row's products per 64-row tile from 256-entry chunks of the tile,
+    jumping over rows of > 256 entries: long rows starting exactly at a chunk edge or at the tile's
+    first entry, empty rows between them, short rows after them."""
+    rng = np.random.default_rng(12)
+    B = from_rows(N, [(r, np.sort(rng.choice(N, rng.integers(1, 5), replace=False))) for r in range(N)], O.U32, rng)
+    sizes = {6400: 256, 6401: 300, 6402: 10, 6403: 0, 6404: 500, 6405: 5, 6406: 251, 6407: 257, 6408: 7,
+             6464: 600, 6465: 3, 6466: 256, 6467: 1000, 6468: 2}
+    rows = [(r, np.sort(rng.choice(N, k, replace=False))) for r, k in sizes.items() if k]
+    taken = set(sizes)
+    rows += [(int(r), np.sort(rng.choice(N, rng.integers(1, 30), replace=False)))
+             for r in range(6300, 6700) if r not in taken]
+    A = from_rows(N, rows, O.U32, rng)
+    assert_same(to_dev(A, slat.CsrMatrix)._spgemm(to_dev(B, slat.CsrMatrix)), O.matmul_seq(A, B), "chunk edges")
