@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -87,6 +88,7 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         delete ctx;
         return SLAT_EOOM;
     }
+    std::memset(ctx->h_out, 0, 64);  // [7] must not match the first call's sequence number
     ctx->d_vmax = ctx->d_words;
     for (auto &e : ctx->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);  // timing only
     *out = ctx;
@@ -572,18 +574,73 @@ static void pick_window(uint64_t ncols, uint32_t threads, uint32_t max_ww, uint3
 
 // End of a call: poll the stream instead of a blocking sync, whose wake-up adds microseconds to
 // every call (SLAT_BLOCKING_SYNC=1 restores the blocking wait)
-static hipError_t wait_stream(hipStream_t s) {
-    static const bool blocking = std::getenv("SLAT_BLOCKING_SYNC") != nullptr;
-    if (blocking) return hipStreamSynchronize(s);
-    hipError_t e;
-    while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+// diagnostics (SLAT_HOST_CLOCK=1): host time of each part of a call, printed every 256 calls:
+// [0] checks, workspace and C allocation, [1] enqueueing the kernels, [2] waiting for them, [3] the rest
+struct HostClock {
+    static bool on() {
+        static const bool e = std::getenv("SLAT_HOST_CLOCK") != nullptr;
+        return e;
     }
-    return e;
+    std::chrono::steady_clock::time_point t;
+    void start() {
+        if (on()) t = std::chrono::steady_clock::now();
+    }
+    void mark(int i) {
+        if (!on()) return;
+        static thread_local double acc[4];
+        const auto now = std::chrono::steady_clock::now();
+        acc[i] += std::chrono::duration<double, std::micro>(now - t).count();
+        t = now;
+        static thread_local long calls = 0;
+        if (i == 3 && ++calls % 256 == 0) {
+            std::fprintf(stderr, "host us/call: setup %.2f enqueue %.2f wait %.2f finish %.2f\n", acc[0] / 256,
+                         acc[1] / 256, acc[2] / 256, acc[3] / 256);
+            acc[0] = acc[1] = acc[2] = acc[3] = 0;
+        }
+    }
+};
+
+__global__ void k_signal(unsigned long long *word, unsigned long long v) {
+    __hip_atomic_store(word, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wait for the call's kernels. Default: a one-thread kernel queued after them stores a sequence
+// number into the context's mapped host words, and the host spins on that word. Measured on this
+// runtime (tools/repro/launch_latency.hip, 4 small kernels per call): 15.2 us per call, against 17.6
+// for hipStreamSynchronize and 27.6 for a hipStreamQuery spin (each query slows the runtime down).
+// Every 2^16 polls the stream is queried, so a faulted kernel surfaces as an error, not a hang.
+// SLAT_WAIT=sync | query selects the other two (A/B only).
+static hipError_t wait_stream(slat_ctx *ctx, hipStream_t s) {
+    static const int mode = [] {
+        const char *e = std::getenv("SLAT_WAIT");
+        if (std::getenv("SLAT_BLOCKING_SYNC") || (e && !std::strcmp(e, "sync"))) return 1;
+        return e && !std::strcmp(e, "query") ? 2 : 0;
+    }();
+    hipError_t e;
+    if (mode == 1) return hipStreamSynchronize(s);
+    if (mode == 2) {
+        while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+        }
+        return e;
+    }
+    const unsigned long long seq = ++ctx->done_seq;
+    hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, s, ctx->h_out_dev + 7, seq);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const volatile unsigned long long *w = ctx->h_out + 7;
+    for (uint32_t i = 1; *w != seq; ++i)
+        if ((i & 0xFFFFu) == 0) {
+            e = hipStreamQuery(s);
+            if (e == hipSuccess) return *w == seq ? hipSuccess : hipStreamSynchronize(s);
+            if (e != hipErrorNotReady) return e;
+        }
+    return hipSuccess;
 }
 
 extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
                                             uint64_t row_end, const slat_csr_view *B, slat_csr *C, uint32_t flags) {
     if (!ctx || !C) return SLAT_EINVAL;
+    HostClock hc;
+    hc.start();
     slat_status st;
     if ((st = slat_check_view(ctx, A, "A")) || (st = slat_check_view(ctx, B, "B"))) return st;
     if (A->dtype != B->dtype) return fail(ctx, SLAT_EINVAL, "A and B value types differ");
@@ -803,6 +860,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.c_rp = C->row_ptr;
 
 
+    hc.mark(0);
     if (a.stats || SLAT_PHASES) SLAT_HIP(ctx, hipMemsetAsync(a.shards, 0, shards_b, s));
     asym.counts = a.counts;
     asym.shards = a.shards;
@@ -933,7 +991,9 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
     if (a.stats) SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                              hipMemcpyDeviceToHost, s));
-    SLAT_HIP(ctx, wait_stream(s));
+    hc.mark(1);
+    SLAT_HIP(ctx, wait_stream(ctx, s));
+    hc.mark(2);
     if (SLAT_PHASES) {
         // diagnostic build: per-phase cycles of the numeric kernel, summed over waves
         unsigned long long ph[kPhaseSlots * 64];
@@ -1022,6 +1082,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]);
         S.total_ms = ms + compact_ms;
     }
+    hc.mark(3);
     return SLAT_OK;
 }
 

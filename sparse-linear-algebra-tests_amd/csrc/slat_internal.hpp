@@ -23,7 +23,9 @@ struct slat_ctx {
     size_t ws_bytes = 0;
     unsigned long long *h_shards = nullptr;  // pinned (stats / max-row read-backs)
     unsigned long long *h_out = nullptr;     // mapped pinned: [0] nnz, [1] max row nnz, [2] rows with zeros
-    unsigned long long *h_out_dev = nullptr; // its device alias (written by k_scan_rows / k_numeric)
+    unsigned long long *h_out_dev = nullptr; // its device alias (written by k_scan_rows / k_numeric); [7]: the
+                                             // end-of-call sequence word (k_signal)
+    unsigned long long done_seq = 0;         // last sequence number queued to [7]
     unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
