@@ -127,6 +127,12 @@ const char *slat_status_string(slat_status s);
 const char *slat_last_error(slat_ctx *ctx);
 slat_status slat_get_stats(slat_ctx *ctx, slat_stats *out);
 slat_status slat_sync(slat_ctx *ctx);
+/* MATMUL_PROGRESS (src/graph_csr.rs:10-11, 355-358, 392-408, 465-481): a process-wide switch; while
+ * on, every SpGEMM call prints the reference's pass summary lines to stderr,
+ * "  symbolic: done in <s>s (<rows/s> rows/s)" and "  numeric:  done in ...", from HIP events
+ * around the passes (a device call has no per-row progress to report). Also on when the environment
+ * variable SLAT_MATMUL_PROGRESS is set at first use. Returns the previous setting. */
+int slat_set_matmul_progress(int on);
 
 /* --- matrices ----------------------------------------------------------------------------- */
 slat_status slat_csr_create(slat_ctx *ctx, const slat_csr_view *src, slat_csr *out); /* copy H2D/D2D */

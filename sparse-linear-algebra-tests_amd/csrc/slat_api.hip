@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -123,6 +124,10 @@ slat_status slat_sync(slat_ctx *ctx) {
     SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return SLAT_OK;
 }
+
+static std::atomic<int> g_progress{std::getenv("SLAT_MATMUL_PROGRESS") ? 1 : 0};
+
+extern "C" int slat_set_matmul_progress(int on) { return g_progress.exchange(on ? 1 : 0, std::memory_order_relaxed); }
 
 slat_status slat_get_stats(slat_ctx *ctx, slat_stats *out) {
     if (!ctx || !out) return SLAT_EINVAL;
@@ -633,6 +638,9 @@ static hipError_t wait_stream(slat_ctx *ctx, hipStream_t s) {
             if (e == hipSuccess) return *w == seq ? hipSuccess : hipStreamSynchronize(s);
             if (e != hipErrorNotReady) return e;
         }
+    // the runtime learns of completed work only through its own calls: let it retire the queue now
+    // and then (event timestamps are read after a hipEventSynchronize of their own)
+    if ((seq & 63) == 0 && (e = hipStreamQuery(s)) != hipSuccess && e != hipErrorNotReady) return e;
     return hipSuccess;
 }
 
@@ -775,7 +783,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     };
     const dim3 grid = num_grid(hash ? 2 : 0, num_lds);
     const dim3 hash_grid = hash ? num_grid(batched ? (sorted ? 4 : 3) : 1, hash_lds) : dim3(1);
-    const bool timing = flags & SLAT_FLAG_TIMING;
+    const bool progress = g_progress.load(std::memory_order_relaxed) != 0;
+    const bool timing = (flags & SLAT_FLAG_TIMING) || progress;
 
     // workspace: counts [n] | ablation counts [n] | shards | scan temp | ELL cols | ELL vals | ELL groups
     auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -1068,6 +1077,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     S.dropped_rows = (uint32_t)drops;
     if (timing) {
         float ms = 0;
+        SLAT_HIP(ctx, hipEventSynchronize(ctx->ev[3]));  // the wait above does not tell the runtime
         (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
         S.symbolic_ms = ms;
         (void)hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]);
@@ -1081,6 +1091,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         }
         (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]);
         S.total_ms = ms + compact_ms;
+    }
+    if (progress) {  // the reference's pass summaries (rows of this call)
+        const double rows = (double)n, ts = S.symbolic_ms * 1e-3, tn = (S.numeric_ms + S.compact_ms) * 1e-3;
+        std::fprintf(stderr, "\r  symbolic: done in %.1fs (%.0f rows/s)                    \n", ts, rows / std::max(ts, 1e-9));
+        std::fprintf(stderr, "\r  numeric:  done in %.1fs (%.0f rows/s)                    \n", tn, rows / std::max(tn, 1e-9));
     }
     hc.mark(3);
     return SLAT_OK;

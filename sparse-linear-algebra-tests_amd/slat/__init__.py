@@ -14,4 +14,11 @@ __all__ = [
     "Context", "Csr", "CsrF64", "CsrMatrix", "CsrU32", "CsrU64", "DeviceCsr", "HostCsr", "MagnusMatrix", "MagnusMatrixUsize", "StdRng",
     "default_context", "host_from_coo", "host_lattice", "host_random", "host_rmat", "host_thin", "load_edges", "torus_thinned", "torus_thinned_device", "SlatError",
     "build", "lib", "U32", "SAT64", "F64", "DEVICE", "HOST", "FLAG_TIMING", "FLAG_EXACT_ALLOC", "FLAG_STATS", "FLAG_F64_ANY_ORDER", "FLAG_IDX64",
+    "set_matmul_progress",
 ]
+
+
+def set_matmul_progress(on: bool = True) -> bool:
+    """MATMUL_PROGRESS.store(on) (src/graph_csr.rs:10-11): every SpGEMM call then prints the
+    reference's symbolic / numeric pass summaries to stderr. Returns the previous setting."""
+    return bool(lib().slat_set_matmul_progress(1 if on else 0))

@@ -18,7 +18,7 @@ FLAG_TIMING, FLAG_EXACT_ALLOC, FLAG_STATS, FLAG_F64_ANY_ORDER, FLAG_IDX64 = 0x1,
 # Every symbol include/slat.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "slat_ctx_create", "slat_ctx_destroy", "slat_ctx_set_stream", "slat_ctx_stream", "slat_status_string",
-    "slat_last_error", "slat_get_stats", "slat_sync", "slat_csr_create", "slat_csr_to_host", "slat_csr_free",
+    "slat_last_error", "slat_get_stats", "slat_sync", "slat_set_matmul_progress", "slat_csr_create", "slat_csr_to_host", "slat_csr_free",
     "slat_csr_view_of", "slat_csr_max_row_nnz", "slat_spgemm", "slat_spgemm_csr_u32", "slat_spgemm_csr_sat64",
     "slat_spgemm_csr_f64", "slat_spgemm_rowblock", "slat_rng_seed", "slat_rng_next_u64", "slat_rng_next_f64",
     "slat_rng_next_u32", "slat_rng_range_u32", "slat_host_random",
@@ -109,6 +109,7 @@ def lib():
         "slat_status_string": ([C.c_int], C.c_char_p),
         "slat_last_error": ([vp], C.c_char_p),
         "slat_get_stats": ([vp, P(Stats)], C.c_int),
+        "slat_set_matmul_progress": ([C.c_int], C.c_int),
         "slat_sync": ([vp], C.c_int),
         "slat_csr_create": ([vp, P(CsrView), P(CsrOwned)], C.c_int),
         "slat_csr_to_host": ([vp, P(CsrView), vp, vp, vp], C.c_int),

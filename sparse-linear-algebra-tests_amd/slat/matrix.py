@@ -221,6 +221,7 @@ class DeviceCsr:
         self._m = owned
         self._ctx = ctx
         self._host = None
+        self._view = None  # the matrix is immutable between in-place replacements (permute)
 
     def __del__(self):
         try:
@@ -352,6 +353,7 @@ class DeviceCsr:
         L.lib().slat_csr_free(self._ctx.ptr, C.byref(self._m))
         self._m = out
         self._host = None
+        self._view = None
         self.perm = p.copy()
 
     def rcm(self):
@@ -409,6 +411,12 @@ class DeviceCsr:
     def view(self) -> L.CsrView:
         return L.lib().slat_csr_view_of(C.byref(self._m))
 
+    def _cview(self) -> L.CsrView:
+        """The view, cached for the product calls (never handed out: callers may edit a view)."""
+        if self._view is None:
+            self._view = self.view()
+        return self._view
+
     def host(self) -> HostCsr:
         if self._host is None:
             n, z, dt = self.n, self.nnz(), int(self._m.dtype)
@@ -450,7 +458,7 @@ class DeviceCsr:
     def _spgemm(self, other: "DeviceCsr", flags: int = 0):
         if type(other) is not type(self):
             raise TypeError("operands must have the same matrix type")
-        a, b = self.view(), other.view()
+        a, b = self._cview(), other._cview()
         out = L.CsrOwned()
         L.check(L.lib().slat_spgemm(self._ctx.ptr, C.byref(a), C.byref(b), C.byref(out), flags), self._ctx.ptr)
         return type(self)(out, self._ctx)
@@ -506,7 +514,7 @@ class DeviceCsr:
         return type(self)(out, self._ctx)
 
     def matmul_rowblock(self, row_begin: int, row_end: int, other: "DeviceCsr", flags: int = 0):
-        a, b = self.view(), other.view()
+        a, b = self._cview(), other._cview()
         out = L.CsrOwned()
         L.check(L.lib().slat_spgemm_rowblock(self._ctx.ptr, C.byref(a), row_begin, row_end, C.byref(b),
                                              C.byref(out), flags), self._ctx.ptr)

@@ -318,3 +318,18 @@ def test_u32_csr_walk_narrow_and_hub_rows(ctx, vmax, wide):
     b = O.from_coo(n, b_rows, b_cols, g.integers(1, vmax + 1, len(b_rows)), O.U32)
     got = to_dev(a, slat.U32).matmul(to_dev(b, slat.U32))
     assert_same(got, O.matmul_seq(a, b), f"csr walk vmax={vmax} wide={wide}")
+
+
+def test_matmul_progress_lines(ctx, capfd):
+    """MATMUL_PROGRESS (src/graph_csr.rs:10-11, 404-408, 477-481): the pass summary lines on stderr."""
+    a = slat.torus_thinned_device(10, 3.0, slat.StdRng(), ctx)
+    prev = slat.set_matmul_progress(True)
+    try:
+        c = a.matmul_par(a)
+    finally:
+        slat.set_matmul_progress(prev)
+    err = capfd.readouterr().err
+    assert "  symbolic: done in " in err and "  numeric:  done in " in err and "rows/s)" in err
+    assert c.nnz() > 0
+    a.matmul_par(a)
+    assert "symbolic:" not in capfd.readouterr().err  # off again
