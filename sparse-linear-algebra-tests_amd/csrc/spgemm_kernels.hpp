@@ -1903,14 +1903,14 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
 // Wave-wide bitonic sort of 256 (key, payload) pairs, 4 per lane (element i = lane * 4 + e): the
 // emit order of the hash categories' keys (and the sorted short-row experiment, short_sort.hpp).
 // ------------------------------------------------------------------------------------------------
-// value of lane (lane ^ M): DPP quad permutes for 1 and 2, ds_swizzle (bit-mask mode, within 32
-// lanes) up to 16, ds_bpermute for 32
+// value of lane (lane ^ M): DPP quad permutes for 1 and 2 (bound_ctrl: no old value to set up, every
+// lane reads a valid source), ds_swizzle (bit-mask mode, within 32 lanes) up to 16, ds_bpermute for 32
 template <int M>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
     if constexpr (M == 1)
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
     else if constexpr (M == 2)
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, true);  // quad_perm [2,3,0,1]
     else if constexpr (M < 32)
         return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (M << 10) | 0x1F);
     else
@@ -1927,22 +1927,25 @@ __device__ __forceinline__ T lane_xor_t(T v) {
 }
 
 // One compare-exchange step (K, J) of the bitonic network over 256 elements, element i = lane * 4 + e.
-// Ties keep their own payload, so the pair never duplicates or loses one.
-template <int K, int J, bool HV, typename T>
+// U (unique keys, or ties whose payloads do not matter: the emit's kSent padding): a swap is one
+// compare xor'ed with the lane's direction mask. Otherwise ties keep their own payload, so a pair
+// never duplicates or loses one.
+template <int K, int J, bool HV, bool U, typename T>
 __device__ __forceinline__ void bitonic_step(uint32_t (&k)[4], T (&v)[4], uint32_t lane) {
     if constexpr (J >= 4) {
         constexpr int M = J / 4;
         const bool asc = (lane & (K / 4)) == 0;
         const bool tmin = ((lane & M) == 0) == asc;
+        uint32_t pk[4];
+        T pv[4];
         sfor<4>([&](auto E) {
-            constexpr int e = decltype(E)::value;
-            const uint32_t pk = lane_xor<M>(k[e]);
-            const bool sw = tmin ? pk < k[e] : pk > k[e];
-            if constexpr (HV) {
-                const T pv = lane_xor_t<M>(v[e]);
-                v[e] = sw ? pv : v[e];
-            }
-            k[e] = sw ? pk : k[e];
+            pk[E] = lane_xor<M>(k[E]);
+            if constexpr (HV) pv[E] = lane_xor_t<M>(v[E]);
+        });
+        sfor<4>([&](auto E) {
+            const bool sw = U ? ((pk[E] < k[E]) == tmin) : (tmin ? pk[E] < k[E] : pk[E] > k[E]);
+            if constexpr (HV) v[E] = sw ? pv[E] : v[E];
+            k[E] = sw ? pk[E] : k[E];
         });
     } else {
         sfor<4>([&](auto E) {
@@ -1950,7 +1953,7 @@ __device__ __forceinline__ void bitonic_step(uint32_t (&k)[4], T (&v)[4], uint32
             if constexpr ((e & J) == 0) {
                 constexpr int f = e | J;
                 const bool asc = (((lane << 2) | (uint32_t)e) & (uint32_t)K) == 0;
-                const bool sw = asc ? k[e] > k[f] : k[e] < k[f];
+                const bool sw = U ? ((k[f] < k[e]) == asc) : (asc ? k[e] > k[f] : k[e] < k[f]);
                 const uint32_t t = k[e];
                 k[e] = sw ? k[f] : t;
                 k[f] = sw ? t : k[f];
@@ -1963,23 +1966,23 @@ __device__ __forceinline__ void bitonic_step(uint32_t (&k)[4], T (&v)[4], uint32
         });
     }
 }
-template <int K, int J, bool HV, typename T>
+template <int K, int J, bool HV, bool U, typename T>
 __device__ __forceinline__ void bitonic_merge(uint32_t (&k)[4], T (&v)[4], uint32_t lane) {
-    bitonic_step<K, J, HV, T>(k, v, lane);
-    if constexpr (J > 1) bitonic_merge<K, J / 2, HV, T>(k, v, lane);
+    bitonic_step<K, J, HV, U, T>(k, v, lane);
+    if constexpr (J > 1) bitonic_merge<K, J / 2, HV, U, T>(k, v, lane);
 }
 // ascending sort of the wave's 256 keys (kSent last), payloads travel with their keys
-template <bool HV, typename T>
+template <bool HV, typename T, bool U = false>
 __device__ __forceinline__ void wave_sort256(uint32_t (&k)[4], T (&v)[4]) {
     const uint32_t lane = (uint32_t)lane_id();
-    bitonic_merge<2, 1, HV, T>(k, v, lane);
-    bitonic_merge<4, 2, HV, T>(k, v, lane);
-    bitonic_merge<8, 4, HV, T>(k, v, lane);
-    bitonic_merge<16, 8, HV, T>(k, v, lane);
-    bitonic_merge<32, 16, HV, T>(k, v, lane);
-    bitonic_merge<64, 32, HV, T>(k, v, lane);
-    bitonic_merge<128, 64, HV, T>(k, v, lane);
-    bitonic_merge<256, 128, HV, T>(k, v, lane);
+    bitonic_merge<2, 1, HV, U, T>(k, v, lane);
+    bitonic_merge<4, 2, HV, U, T>(k, v, lane);
+    bitonic_merge<8, 4, HV, U, T>(k, v, lane);
+    bitonic_merge<16, 8, HV, U, T>(k, v, lane);
+    bitonic_merge<32, 16, HV, U, T>(k, v, lane);
+    bitonic_merge<64, 32, HV, U, T>(k, v, lane);
+    bitonic_merge<128, 64, HV, U, T>(k, v, lane);
+    bitonic_merge<256, 128, HV, U, T>(k, v, lane);
 }
 
 // LDS of k_numeric_short per wave: the hash table of ShortSem<Sem> (hash_bytes: keys | values |
@@ -2030,7 +2033,7 @@ __device__ __forceinline__ void batch_emit(uint32_t *hkeys, typename Sem::V *hva
     sfor<4>([&](auto E) {
         if (lane * 4 + E >= nk) k[E] = kSent;
     });
-    wave_sort256<true, uint32_t>(k, sl);
+    wave_sort256<true, uint32_t, true>(k, sl);  // distinct keys (kSent padding aside)
     const uint32_t cmask = cb ? (1u << cb) - 1 : 0xFFFFFFFFu;
     sfor<4>([&](auto E) {
         const uint32_t i = lane * 4 + E;
