@@ -333,11 +333,12 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
                                                        uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng,
                                                        unsigned long long *vmax, uint32_t epoch) {
     // one thread per (row k, group t): 4 columns and 4 values, written as whole groups
+    // 32-bit group index: the host keeps n < 2^24 and wq <= 8 for the ELL copy
     uint32_t mx = 0, mn = 0xFFFFFFFFu;
-    const uint64_t total = (uint64_t)n * wq;
-    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t k = g / wq;
-        const uint32_t t = (uint32_t)(g - k * wq);
+    const uint32_t total = n * wq;
+    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < total; g += gridDim.x * kBlock) {
+        const uint32_t k = g / wq;
+        const uint32_t t = g - k * wq;
         const uint64_t s0 = rp[k], len = rp[k + 1] - s0;
         if (t == 0) eng[k] = (uint8_t)((len + 3) / 4);
         uint32_t c[4];
@@ -354,8 +355,13 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
                 }
         }
         ((uint4 *)ecol)[g] = make_uint4(c[0], c[1], c[2], c[3]);
+        if constexpr (sizeof(S) == 4) {
+            ((uint4 *)eval)[g] = make_uint4(__builtin_bit_cast(uint32_t, v[0]), __builtin_bit_cast(uint32_t, v[1]),
+                                            __builtin_bit_cast(uint32_t, v[2]), __builtin_bit_cast(uint32_t, v[3]));
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) eval[g * 4 + e] = v[e];
+            for (int e = 0; e < 4; ++e) eval[(uint64_t)g * 4 + e] = v[e];
+        }
     }
     if constexpr (std::is_same<S, uint32_t>::value) {
         // max and min B value, one atomic each per block (the min as max of ~v); the epoch in the

@@ -7,6 +7,12 @@
 __global__ void k_touch(unsigned *x, unsigned v) {
     if (threadIdx.x == 0 && blockIdx.x == 0) x[0] = v;
 }
+struct Big {
+    unsigned long long w[40];  // 320 B of kernel arguments, like the library's Args
+};
+__global__ void k_big(Big b, unsigned *x) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) x[0] = (unsigned)b.w[3];
+}
 __global__ void k_flag(volatile unsigned *host_flag, unsigned v) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         __threadfence_system();
@@ -64,5 +70,21 @@ int main() {
     for (int i = 0; i < iters; ++i) { for (int k = 0; k < 4; ++k) hipLaunchKernelGGL(k_touch, dim3(1), dim3(64), 0, s, d, i); }
     CK(hipStreamSynchronize(s));
     std::printf("enqueue only, 4 kernels: %.2f us/call\n", (now_us() - t0) / iters);
+    Big b{};
+    t0 = now_us();
+    for (int i = 0; i < iters; ++i) {
+        b.w[3] = i;
+        for (int k = 0; k < 4; ++k) hipLaunchKernelGGL(k_big, dim3(64), dim3(256), 0, s, b, d);
+    }
+    CK(hipStreamSynchronize(s));
+    std::printf("enqueue only, 4 kernels with 320-byte arguments: %.2f us/call\n", (now_us() - t0) / iters);
+    t0 = now_us();
+    for (int i = 0; i < iters; ++i) {
+        b.w[3] = i;
+        for (int k = 0; k < 3; ++k) hipLaunchKernelGGL(k_big, dim3(64), dim3(256), 0, s, b, d);
+        hipLaunchKernelGGL(k_flag, dim3(1), dim3(64), 0, s, hd, (unsigned)(i + 1));
+        while (((volatile unsigned *)h)[0] != (unsigned)(i + 1)) {}
+    }
+    std::printf("3 kernels with 320-byte arguments + flag kernel, spin: %.2f us/call\n", (now_us() - t0) / iters);
     return 0;
 }
