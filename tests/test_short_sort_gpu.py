@@ -184,3 +184,18 @@ def test_row_bounds_with_long_rows_at_chunk_edges():
              for r in range(6300, 6700) if r not in taken]
     A = from_rows(N, rows, O.U32, rng)
     assert_same(to_dev(A, slat.CsrMatrix)._spgemm(to_dev(B, slat.CsrMatrix)), O.matmul_seq(A, B), "chunk edges")
+
+
+def test_register_sort_experiment_path():
+    """The opt-in register-sorted category (SLAT_SORT_SHORT=1 is read once per process): the edge cases
+    above in a child process with it on."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, SLAT_SORT_SHORT="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(here, "test_short_sort_gpu.py"), "-k",
+                        "category_edges or zeros_and_saturation or sat64_saturating or chunk_edges or one_row_per_batch"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
