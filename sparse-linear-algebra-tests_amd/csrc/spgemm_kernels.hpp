@@ -618,6 +618,11 @@ struct SemU32W {
     }
     __device__ static __forceinline__ bool is_zero(S v) { return v == 0; }
 };
+// SemU32W for a batch whose sums cannot reach 2^32 (max A x max B x groups < 2^32): plain adds, no
+// returned value to test for a wrap, so the atomics pipeline freely (the same slots and wrap words)
+struct SemU32WN : SemU32W {
+    __device__ static __forceinline__ void acc(V *vals, uint32_t r, P p) { atomicAdd(&vals[r], p); }
+};
 template <typename Sem, typename = void>
 struct ExtraWords : std::integral_constant<uint32_t, 0> {};
 template <typename Sem>
@@ -2173,6 +2178,15 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
             pc.mark(1);  // A entries, local rows, group counts
             uint32_t pos[kRegQ];
             const uint32_t G = group_positions(ng, pos);
+            bool narrow = false;  // u32: no sum of this batch can wrap (each key takes <= G products)
+            if constexpr (std::is_same_v<Sem, SemU32W>) {
+                if (bvmax) {
+                    uint32_t am = 0;
+                    sfor<kRegQ>([&](auto Q) { am = max(am, (uint32_t)aq[Q]); });
+                    const unsigned long long ab = (unsigned long long)wave_max_u32(am) * bvmax;
+                    narrow = ab < (1ull << 32) && ab * G < (1ull << 32);
+                }
+            }
             for (uint32_t base = 0; base < G; base += kStageG) {
                 stage_groups<true, S>(base, mxg, kq, lq, ng, pos, aq, gk, gl, ga);
                 const uint32_t n = min(G - base, kStageG);
@@ -2191,7 +2205,15 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
                         ck.z = c.z != kSent ? (hi | c.z) : kSent;
                         ck.w = c.w != kSent ? (hi | c.w) : kSent;
                     }
-                    ha(ck, pr);
+                    if constexpr (std::is_same_v<Sem, SemU32W>) {
+                        if (narrow) {
+                            HashAcc<SemU32WN>{hkeys, hvals}(ck, pr);
+                        } else {
+                            ha(ck, pr);
+                        }
+                    } else {
+                        ha(ck, pr);
+                    }
                 }
                 wave_sync();
             }
