@@ -258,6 +258,33 @@ def test_rank_chunks_long_output_rows(ctx):
         assert_same(to_dev(a, dt)._spgemm(to_dev(b, dt)), O.matmul_seq(a, b), f"chunks dt={dt}")
 
 
+@pytest.mark.parametrize("dt", [slat.U32, slat.SAT64, slat.F64])
+def test_compacted_bitmap_block_groups(ctx, dt):
+    # 60,000 columns: one window of 30 blocks (2048 columns each). Numeric keeps only a row's touched
+    # blocks in LDS, at most 8 per pass: rows touching 1, 7, 8, 9, 16, 17 and all 30 blocks, through
+    # B = I (C = A exactly) and through a random B (outputs spread over every block)
+    rng = np.random.default_rng(11)
+    n = 60000
+    rows, cols = [], []
+    for r, nb in enumerate([1, 7, 8, 9, 16, 17, 30, 0, 3, 30, 12, 8, 9]):
+        blocks = rng.choice(30, nb, replace=False) if nb < 30 else np.arange(30)
+        for b in blocks:
+            k = int(rng.integers(1, 6))
+            c = np.unique(np.minimum(b * 2048 + rng.integers(0, 2048, k), n - 1))
+            rows += [r] * len(c)
+            cols += list(c)
+    more = rng.integers(0, n, 3000)
+    rows += list(20 + (more % 400))
+    cols += list(rng.integers(0, n, 3000))
+    a = O.convert(O.from_coo(n, rows, cols, rng.integers(1, 9, len(rows)), O.U32), DT[dt])
+    eye = O.convert(O.from_coo(n, np.arange(n), np.arange(n), np.ones(n), O.U32), DT[dt])
+    B = O.convert(O.from_coo(n, rng.integers(0, n, 3 * n), rng.integers(0, n, 3 * n),
+                             rng.integers(1, 9, 3 * n), O.U32), DT[dt])
+    da = to_dev(a, dt)
+    assert_same(da._spgemm(to_dev(eye, dt)), O.matmul_seq(a, eye), f"A*I dt={dt}")
+    assert_same(da._spgemm(to_dev(B, dt)), O.matmul_seq(a, B), f"A*B dt={dt}")
+
+
 def test_wide_windows_torus46(ctx):
     # n = 97,336 columns > one 63,488-column window: rows iterate windows from their min column
     rng = O.Rng()
