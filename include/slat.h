@@ -189,6 +189,29 @@ slat_status slat_magnus_to_host(slat_ctx *ctx, const slat_magnus *m, uint64_t *r
                                 uint64_t *values);
 slat_magnus_view slat_magnus_view_of(const slat_magnus *m);
 
+/* --- CsrBTreeMatrix in its own layout (src/graph_csr_btree.rs:44-52) -----------------------------
+ * DenseBTreeList (src/dense_btree.rs:269-330) packs each row as [internal separator nodes | sorted
+ * data] into one flat `nodes` Vec<NodeId>. Row r's columns are nodes[data_off[r] ..
+ * data_off[r] + (data_start[r+1] - data_start[r])), with data_off[r] = its NodeEntry's offset +
+ * internal_len, and its values are values[data_start[r] ..] (data_start[r] = NodeEntry::data_start,
+ * data_start[n_rows] = total_data_len() = nnz). slat_spgemm_btree replaces CsrBTreeMatrix::matmul_par
+ * (src/graph_csr_btree.rs:350-479): the columns are gathered into CSR order on the device, the u32
+ * SpGEMM runs, and C is returned as CSR, the arrays matmul_par passes to from_flat (:99). A slice
+ * outside nodes / nnz or a column >= n_cols -> SLAT_EINVAL. */
+typedef struct {
+    uint64_t n_rows, n_cols, nnz, n_nodes;
+    const uint64_t *data_start; /* n_rows + 1 */
+    const uint64_t *data_off;   /* n_rows */
+    const uint32_t *nodes;      /* n_nodes: separators and data of every row */
+    const uint32_t *values;     /* nnz (Val = u32) */
+    int32_t residency;          /* slat_residency, for all four arrays */
+    int32_t _pad;
+    uint64_t max_row_nnz; /* 0 = unknown */
+} slat_btree_view;
+
+slat_status slat_spgemm_btree(slat_ctx *ctx, const slat_btree_view *A, const slat_btree_view *B, slat_csr *C,
+                              uint32_t flags);
+
 /* --- multi-GPU row blocks over RCCL -------------------------------------------
  * One process per GPU. The reference splits matmul_par's output rows over rayon threads
  * (src/graph_csr.rs:350-484); here rank r computes C rows [cuts[r], cuts[r+1]) with

@@ -2267,7 +2267,13 @@ void k_numeric_short_u32(Args p) {
 // aggregate then its inclusive prefix in an epoch-tagged status word (no init kernel). The last
 // tile writes the total nnz and the max row nnz into mapped host memory (no copy in the stream).
 // ------------------------------------------------------------------------------------------------
-constexpr int kScanThreads = 256, kScanItems = 8;
+#ifndef SLAT_SCAN_THREADS
+#define SLAT_SCAN_THREADS 256  // variant builds: tile geometry of k_scan_rows
+#endif
+#ifndef SLAT_SCAN_ITEMS
+#define SLAT_SCAN_ITEMS 8
+#endif
+constexpr int kScanThreads = SLAT_SCAN_THREADS, kScanItems = SLAT_SCAN_ITEMS;
 constexpr uint64_t kScanTile = (uint64_t)kScanThreads * kScanItems;
 constexpr unsigned long long kStAgg = 1ull << 40, kStInc = 2ull << 40, kStVal = (1ull << 40) - 1;
 

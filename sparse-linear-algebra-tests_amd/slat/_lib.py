@@ -29,7 +29,7 @@ EXPORTS = [
     "slat_bandwidth_stats", "slat_spgemm_dense", "slat_device_alloc", "slat_device_free", "slat_device_copy",
     "slat_magnus_matmul", "slat_magnus_free", "slat_magnus_to_host", "slat_magnus_view_of",
     "slat_comm_id", "slat_comm_create", "slat_comm_destroy", "slat_rowblock_cuts", "slat_bcast_csr",
-    "slat_allgather_rows", "slat_diameter",
+    "slat_allgather_rows", "slat_diameter", "slat_spgemm_btree",
 ]
 
 
@@ -62,6 +62,12 @@ class MagnusOwned(C.Structure):
     _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_uint64), ("nnz", C.c_uint64), ("capacity", C.c_uint64),
                 ("max_row_nnz", C.c_uint64), ("row_ptr", C.c_void_p), ("col_idx", C.c_void_p),
                 ("values", C.c_void_p), ("device", C.c_int32), ("_pad", C.c_int32), ("_owner", C.c_uint8 * 96)]
+
+
+class BTreeView(C.Structure):
+    _fields_ = [("n_rows", C.c_uint64), ("n_cols", C.c_uint64), ("nnz", C.c_uint64), ("n_nodes", C.c_uint64),
+                ("data_start", C.c_void_p), ("data_off", C.c_void_p), ("nodes", C.c_void_p), ("values", C.c_void_p),
+                ("residency", C.c_int32), ("_pad", C.c_int32), ("max_row_nnz", C.c_uint64)]
 
 
 class Stats(C.Structure):
@@ -162,6 +168,7 @@ def lib():
         "slat_bcast_csr": ([vp, vp, P(CsrOwned), C.c_int], C.c_int),
         "slat_allgather_rows": ([vp, vp, P(CsrView), P(CsrOwned)], C.c_int),
         "slat_diameter": ([vp, P(CsrView), P(u64), P(u64), P(u64)], C.c_int),
+        "slat_spgemm_btree": ([vp, P(BTreeView), P(BTreeView), P(CsrOwned), u32], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

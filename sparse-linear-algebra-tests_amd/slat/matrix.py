@@ -636,3 +636,74 @@ class CsrU64(Csr):
 
 class CsrF64(Csr):
     DTYPE = L.F64
+
+
+class CsrBTreeMatrix:
+    """`CsrBTreeMatrix` (src/graph_csr_btree.rs:44-52) in its host layout: DenseBTreeList's flat
+    `nodes` (every row as [separator nodes | sorted data], src/dense_btree.rs:269-330), the flat
+    `values`, and per row data_start (NodeEntry::data_start, plus total_data_len() at the end) and
+    data_off (offset + internal_len). matmul_par runs on the MI355X engine through
+    slat_spgemm_btree, which reads only the data slices.
+
+    The separators built here are a one-level index (every 16th key of the row after the first),
+    a stand-in for DenseBTree::extend_from_sorted's levels: the engine never reads them, and the
+    tests only need them to sit between the rows' data as in the reference's layout."""
+
+    def __init__(self, n: int, nodes, values, data_start, data_off, ctx: Context | None = None):
+        self.n = int(n)
+        self.nodes = np.ascontiguousarray(nodes, np.uint32)
+        self.values = np.ascontiguousarray(values, np.uint32)
+        self.data_start = np.ascontiguousarray(data_start, np.uint64)
+        self.data_off = np.ascontiguousarray(data_off, np.uint64)
+        self._ctx = ctx or default_context()
+
+    @classmethod
+    def from_flat(cls, n: int, row_ptr, col_idx, values, ctx: Context | None = None) -> "CsrBTreeMatrix":
+        """CsrBTreeMatrix::from_flat (src/graph_csr_btree.rs:57-63): one tree per row, in row order."""
+        row_ptr = np.asarray(row_ptr, np.uint64)
+        col_idx = np.asarray(col_idx, np.uint32)
+        parts, offs, pos = [], np.zeros(n, np.uint64), 0
+        for r in range(n):
+            data = col_idx[int(row_ptr[r]):int(row_ptr[r + 1])]
+            sep = data[16::16]
+            parts += [sep, data]
+            offs[r] = pos + len(sep)
+            pos += len(sep) + len(data)
+        nodes = np.concatenate(parts) if parts else np.zeros(0, np.uint32)
+        return cls(n, nodes, values, row_ptr, offs, ctx)
+
+    @classmethod
+    def from_host(cls, h: HostCsr, ctx: Context | None = None) -> "CsrBTreeMatrix":
+        return cls.from_flat(h.n, h.row_ptr, h.col_idx, h.values, ctx)
+
+    def nnz(self) -> int:
+        return int(self.data_start[self.n])
+
+    def data(self, r: int) -> np.ndarray:
+        """DenseBTreeList::data (src/dense_btree.rs:311-314): the sorted columns of row r."""
+        o = int(self.data_off[r])
+        return self.nodes[o:o + int(self.data_start[r + 1] - self.data_start[r])]
+
+    def view(self) -> L.BTreeView:
+        v = L.BTreeView()
+        v.n_rows = v.n_cols = self.n
+        v.nnz = self.nnz()
+        v.n_nodes = len(self.nodes)
+        v.data_start = self.data_start.ctypes.data
+        v.data_off = self.data_off.ctypes.data
+        v.nodes = self.nodes.ctypes.data
+        v.values = self.values.ctypes.data
+        v.residency = L.HOST
+        return v
+
+    def matmul_par_csr(self, other: "CsrBTreeMatrix") -> CsrMatrix:
+        """CsrBTreeMatrix::matmul_par (src/graph_csr_btree.rs:350-479) up to its from_flat: the
+        product as a device CsrMatrix."""
+        a, b, out = self.view(), other.view(), L.CsrOwned()
+        L.check(L.lib().slat_spgemm_btree(self._ctx.ptr, C.byref(a), C.byref(b), C.byref(out), 0), self._ctx.ptr)
+        return CsrMatrix(out, self._ctx)
+
+    def matmul_par(self, other: "CsrBTreeMatrix") -> "CsrBTreeMatrix":
+        """CsrBTreeMatrix::matmul_par, the output's trees built on the host as the reference does."""
+        h = self.matmul_par_csr(other).host()
+        return CsrBTreeMatrix.from_flat(self.n, h.row_ptr, h.col_idx, h.values, self._ctx)

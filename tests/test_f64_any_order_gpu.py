@@ -55,3 +55,24 @@ def test_any_order_exact_cancellation_dropped(ctx):
     got = da._spgemm(db, slat.FLAG_F64_ANY_ORDER)
     want = O.matmul_seq(A, B)
     check(got, want, "cancellation")
+
+
+def test_rmat_scale18_c5_size(ctx):
+    # SURVEY §8(d) C5 at its stated size: R-MAT 2^18 rows, degree 16 (1.28 G outputs). The
+    # reference's fold order bit-exact and the any-order mode within rtol 1e-12, both against one
+    # oracle product (matmul_par, 16 threads)
+    h = slat.host_rmat(18, (1 << 18) * 16)
+    o = O.from_arrays(h.row_ptr, h.col_idx, h.values, O.F64)
+    d = slat.CsrF64.from_host(h)
+    del h
+    want = O.matmul_par(o, o, 16)
+    rp, col, val = want.arrays()
+    for flags in (0, slat.FLAG_F64_ANY_ORDER):
+        got = d._spgemm(d, flags).host()
+        np.testing.assert_array_equal(got.row_ptr, rp, err_msg=f"scale 18 flags={flags} row_ptr")
+        np.testing.assert_array_equal(got.col_idx, col, err_msg=f"scale 18 flags={flags} col_idx")
+        if flags:
+            np.testing.assert_allclose(got.values, val, rtol=RTOL, atol=0, err_msg="scale 18 any order")
+        else:
+            np.testing.assert_array_equal(got.values.view(np.uint64), val.view(np.uint64), err_msg="scale 18 fold bits")
+        del got
