@@ -617,11 +617,13 @@ __global__ void k_signal(unsigned long long *word, unsigned long long v) {
 // runtime (tools/repro/launch_latency.hip, 4 small kernels per call): 15.2 us per call, against 17.6
 // for hipStreamSynchronize and 27.6 for a hipStreamQuery spin (each query slows the runtime down).
 // Every 2^16 polls the stream is queried, so a faulted kernel surfaces as an error, not a hang.
-// SLAT_WAIT=sync | query selects the other two (A/B only).
+// SLAT_WAIT=sync | query selects the other two, SLAT_WAIT=write stores the word with
+// hipStreamWriteValue64 instead of k_signal (A/B only).
 static hipError_t wait_stream(slat_ctx *ctx, hipStream_t s) {
     static const int mode = [] {
         const char *e = std::getenv("SLAT_WAIT");
         if (std::getenv("SLAT_BLOCKING_SYNC") || (e && !std::strcmp(e, "sync"))) return 1;
+        if (e && !std::strcmp(e, "write")) return 3;  // the sequence word stored by a stream write op
         return e && !std::strcmp(e, "query") ? 2 : 0;
     }();
     hipError_t e;
@@ -632,8 +634,12 @@ static hipError_t wait_stream(slat_ctx *ctx, hipStream_t s) {
         return e;
     }
     const unsigned long long seq = ++ctx->done_seq;
-    hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, s, ctx->h_out_dev + 7, seq);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (mode == 3) {
+        if ((e = hipStreamWriteValue64(s, ctx->h_out_dev + 7, seq, 0)) != hipSuccess) return e;
+    } else {
+        hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, s, ctx->h_out_dev + 7, seq);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     const volatile unsigned long long *w = ctx->h_out + 7;
     for (uint32_t i = 1; *w != seq; ++i)
         if ((i & 0xFFFFu) == 0) {
