@@ -520,12 +520,16 @@ static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStre
         hipLaunchKernelGGL((k_symbolic<uint64_t, false>), grid, dim3(kBlock), lds, s, a);
 }
 
+// blocks of k_build_ell (each stores one B-value partial for k_scan_rows when u32)
+static uint32_t build_ell_blocks(const slat_csr_view *B, uint32_t wq) {
+    return (uint32_t)std::max<uint64_t>(std::min<uint64_t>((B->n_rows * wq + kBlock - 1) / kBlock, 4096), 1);
+}
+
 template <typename S>
 static hipError_t launch_build_ell(hipStream_t s, const slat_csr_view *B, uint32_t wq, uint32_t *ecol, void *eval,
-                                   uint8_t *eng, unsigned long long *vmax, uint32_t epoch) {
-    const uint64_t blocks = std::min<uint64_t>((B->n_rows * wq + kBlock - 1) / kBlock, 4096);
-    hipLaunchKernelGGL(k_build_ell<S>, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(kBlock), 0, s, B->row_ptr,
-                       B->col_idx, (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng, vmax, epoch);
+                                   uint8_t *eng, unsigned long long *part) {
+    hipLaunchKernelGGL(k_build_ell<S>, dim3(build_ell_blocks(B, wq)), dim3(kBlock), 0, s, B->row_ptr, B->col_idx,
+                       (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng, part);
     return hipGetLastError();
 }
 
@@ -539,7 +543,8 @@ static hipError_t launch_compact(dim3 grid, hipStream_t s, const uint64_t *orp, 
 
 // row_ptr[0..n] of a count vector: k_scan_rows (one kernel); the total and the max count land in
 // ctx->h_out[0], [1] once the stream reaches that point
-slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s) {
+slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s,
+                             const unsigned long long *bpart, uint32_t nbpart, uint32_t vepoch) {
     const uint64_t tiles = std::max<uint64_t>((n + kScanTile - 1) / kScanTile, 1);
     if (tiles > ctx->status_cap) {
         if (ctx->d_status) slat_dev_free(ctx, ctx->d_status, s);
@@ -555,7 +560,8 @@ slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, 
         ctx->scan_epoch = 1;
     }
     hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status,
-                       ctx->d_words + 1, ctx->ticket_base, ctx->scan_epoch, ctx->d_words + 2, ctx->h_out_dev);
+                       ctx->d_words + 1, ctx->ticket_base, ctx->scan_epoch, ctx->d_words + 2, ctx->h_out_dev, bpart,
+                       nbpart, ctx->d_vmax, vepoch);
     SLAT_HIP(ctx, hipGetLastError());
     ctx->ticket_base += tiles;
     return SLAT_OK;
@@ -822,7 +828,9 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     static const bool kNoFat = std::getenv("SLAT_NO_FAT") != nullptr;
     const uint64_t maxrow_a = A->max_row_nnz;
     const bool fat = !kNoFat && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
-    const size_t o_fat = o_lc + lc_b, fat_b = fat ? slat_fat_ws(n) : 0;
+    // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
+    const size_t o_part = o_lc + lc_b, part_b = (ell && dt == SLAT_U32) ? 4096 * 8 : 0;
+    const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
     if ((st = slat_ensure_ws(ctx, o_fat + fat_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (ell) {
@@ -893,11 +901,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (ell) {
         hipError_t be;
         if (dt == SLAT_U32)
-            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, ctx->d_vmax, a.epoch);
+            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
+                                            (unsigned long long *)(ws + o_part));
         else if (dt == SLAT_SAT64)
-            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, ctx->d_vmax, a.epoch);
+            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
         else
-            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, ctx->d_vmax, a.epoch);
+            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
         SLAT_HIP(ctx, be);
     } else if (a.b_vmax && B->nnz) {
         const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
@@ -959,7 +968,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     SLAT_HIP(ctx, hipGetLastError());
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
-    if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s))) return st;
+    // (u32 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
+    const bool bpart = ell && dt == SLAT_U32;
+    if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
+                               bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
+                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch)))
+        return st;
     if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
 
     if (exact) {

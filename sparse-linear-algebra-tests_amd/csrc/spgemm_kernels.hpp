@@ -331,7 +331,7 @@ __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&
 template <typename S>
 __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const uint32_t *col, const S *val,
                                                        uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng,
-                                                       unsigned long long *vmax, uint32_t epoch) {
+                                                       unsigned long long *part) {
     // one thread per (row k, group t): 4 columns and 4 values, written as whole groups
     // 32-bit group index: the host keeps n < 2^24 and wq <= 8 for the ELL copy
     uint32_t mx = 0, mn = 0xFFFFFFFFu;
@@ -364,8 +364,9 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
         }
     }
     if constexpr (std::is_same<S, uint32_t>::value) {
-        // max and min B value, one atomic each per block (the min as max of ~v); the epoch in the
-        // high word supersedes earlier calls' values without a reset
+        // max and min B value of this block, stored as one partial ((~min << 32) | max) that
+        // k_scan_rows reduces into the epoch-tagged words: no same-address atomics and no
+        // round trip at the end of every block
         __shared__ uint32_t bm[kBlock / kWave], bn[kBlock / kWave];
         mx = wave_max_u32(mx);
         mn = wave_min_u32(mn);
@@ -379,14 +380,7 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
                 mx = max(mx, bm[w]);
                 mn = min(mn, bn[w]);
             }
-            // the words only grow: skip the atomic when the current value already covers ours, so
-            // the blocks of a pattern B (all values equal) do not serialise on one L2 line
-            const unsigned long long wx = ((unsigned long long)epoch << 32) | mx;
-            const unsigned long long wn = ((unsigned long long)epoch << 32) | ~mn;
-            if (__hip_atomic_load(&vmax[kVMaxWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wx)
-                atomicMax(&vmax[kVMaxWord], wx);
-            if (__hip_atomic_load(&vmax[kVMinInvWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wn)
-                atomicMax(&vmax[kVMinInvWord], wn);
+            part[blockIdx.x] = ((unsigned long long)~mn << 32) | mx;
         }
     }
 }
@@ -2287,10 +2281,15 @@ __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long l
     return v;
 }
 
+// bpart (optional): k_build_ell's nbpart per-block B-value partials ((~min << 32) | max), reduced by
+// one wave of tile 0 into vmax[kVMaxWord] = (vepoch << 32) | max, vmax[kVMinInvWord] =
+// (vepoch << 32) | ~min for the numeric pass (which runs after this kernel)
 static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_t *counts, uint64_t n, uint64_t *rp,
                                                             unsigned long long *status, unsigned long long *ticket,
                                                             unsigned long long ticket_base, uint32_t epoch,
-                                                            unsigned long long *maxw, unsigned long long *host_out) {
+                                                            unsigned long long *maxw, unsigned long long *host_out,
+                                                            const unsigned long long *bpart, uint32_t nbpart,
+                                                            unsigned long long *vmax, uint32_t vepoch) {
     __shared__ unsigned long long wsum[kScanThreads / kWave];
     __shared__ unsigned long long s_bcast[2];
     __shared__ uint32_t wmax[kScanThreads / kWave];
@@ -2361,6 +2360,20 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
 #pragma unroll
     for (int e = 0; e < kScanItems; ++e)
         if (i0 + e < n) rp[1 + i0 + e] = pre + v[e];
+    if (tile == 0 && nbpart && w == kScanThreads / kWave - 1) {
+        uint32_t bx = 0, bn = 0;  // max, max of ~min
+        for (uint32_t i = lane; i < nbpart; i += kWave) {
+            const unsigned long long q = bpart[i];
+            bx = max(bx, (uint32_t)q);
+            bn = max(bn, (uint32_t)(q >> 32));
+        }
+        bx = wave_max_u32(bx);
+        bn = wave_max_u32(bn);
+        if (lane == 0) {
+            vmax[kVMaxWord] = ((unsigned long long)vepoch << 32) | bx;
+            vmax[kVMinInvWord] = ((unsigned long long)vepoch << 32) | bn;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
