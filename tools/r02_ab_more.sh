@@ -1,7 +1,7 @@
 #!/bin/bash
 # tree vs tools/bin/libslat_$1.so: bench.py alternated 4 times, then a kernel trace of the tree
 set -o pipefail
-OUT=gpurun_out/ab_more; mkdir -p $OUT
+OUT=gpurun_out/${AB_OUT:-ab_more}; mkdir -p $OUT
 for i in 1 2 3 4; do
   for v in $1 tree; do
     if [ $v = tree ]; then unset SLAT_LIB_PATH; else export SLAT_LIB_PATH=tools/bin/libslat_$v.so; fi
