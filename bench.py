@@ -8,15 +8,20 @@ saturating values, nnz(C) = 11,736,555. Inputs are device-resident before the ti
 step is one complete synchronous SpGEMM call (symbolic, scan, C allocation, numeric, nnz read-back)
 and its output is released inside the step.
 
-N > 1 (torchrun, one rank per GPU): `--scaling strong` (default) — config C4, the 100^3 torus,
-C = A^3·A, whose rows are split across the ranks into flops-balanced blocks cut on the device
-(north_star: >= 6x strong scaling at 8 GPUs). Rank 0 builds A and A^3 and broadcasts them over
-RCCL (libslat's slat_bcast_csr, outside the timed region); each rank then times its row block with
-no data-path collective (C stays row-distributed, the next power's left operand). Rank 0 also times
-the whole product alone on its GPU afterwards and reports the speedup. `--gather` adds the
-allgatherv of C's row blocks over RCCL (slat_allgather_rows), timed separately as gather_ms.
-`--scaling weak` is the labelled extra: one 30^3 torus per rank (the block-diagonal matrix).
-value = output nnz of all ranks / max-over-ranks time.
+N > 1 (torchrun, one rank per GPU): `--scaling weak` (default) — the same workload on every rank (one
+30^3 torus per rank, the block-diagonal matrix: the path partitions into independent row blocks with
+no data-path collective), value = all ranks' output nnz / max-over-ranks time, so the driver's
+1/2/4/8 curve compares one metric on one workload. Every run (N = 1 included) also carries the
+north_star strong-scaling leg on config C4 (100^3 torus, C = A^3 * A) in config.c4: the product's
+rows split into flops-balanced blocks cut on the device, B and the left operand broadcast over RCCL
+from rank 0 (slat_bcast_csr, untimed), each rank timing its block; the blocks are then assembled
+over RCCL (slat_allgather_rows, timed apart as gather_ms) and rank 0 checks the gathered product
+against the golden digests (tests/golden/golden.json); rank 0 also times the whole C4 product alone
+(single_gpu_ms), so c4.speedup is a same-run strong-scaling figure. `--scaling strong` makes the C4
+leg the headline value instead.
+
+Parity: rank 0 digests one timed-workload output (outside the timed region) against the golden
+SHA-256 of the same power ("parity": true | false in the JSON line).
 
 Prints ONE JSON line on rank 0.
 """
@@ -86,6 +91,120 @@ def load_pmc(workload: str):
     return None
 
 
+def golden(side: int, power: int):
+    """The golden digests (tests/golden/golden.json, made by tests/golden/make_golden.py) of A^power
+    on the side^3 torus, or None."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            g = json.load(f)
+    except OSError:
+        return None
+    for e in g.get(f"torus{side}_powers", []):
+        if e.get("k") == power:
+            return e
+    return None
+
+
+def parity(C, side: int, power: int):
+    """C's row_ptr / col_idx / values SHA-256 against the golden digests (u32 values)."""
+    import hashlib
+    want = golden(side, power)
+    if want is None:
+        return None
+    h = C.host()
+    got = {"row_ptr": hashlib.sha256(np.asarray(h.row_ptr, dtype="<u8").tobytes()).hexdigest(),
+           "col": hashlib.sha256(np.asarray(h.col_idx, dtype="<u4").tobytes()).hexdigest(),
+           "val": hashlib.sha256(np.asarray(h.values, dtype="<u4").tobytes()).hexdigest()}
+    return int(C.nnz()) == want["nnz"] and all(got[k] == want[k] for k in got)
+
+
+def timed_steps(run, steps, warmup, barrier):
+    for _ in range(warmup):
+        run()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    barrier()
+    return time.perf_counter() - t0
+
+
+def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
+    """North_star strong scaling on config C4 (100^3 torus, C = A^3 * A): flops-balanced row blocks
+    over the ranks, B and the left operand broadcast from rank 0; then the blocks' allgatherv over
+    RCCL and the golden check on rank 0, and the whole product alone on rank 0's GPU."""
+    side, power = 100, 4
+    if comm is not None:
+        A, P = build_inputs(side, power, ctx) if rank == 0 else (None, None)
+        A = comm.bcast(A, slat.CsrMatrix)
+        P = comm.bcast(P, slat.CsrMatrix)
+    else:
+        A, P = build_inputs(side, power, ctx)
+    n = A.n
+    cuts = slat_dist.device_cuts(P, A, world) if world > 1 else [0, n]
+    lo, hi = cuts[rank], cuts[rank + 1]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        ctx.sync()
+
+    nz = [0]
+
+    def run():
+        C = P.matmul_rowblock(lo, hi, A, 0)
+        nz[0] = C.nnz()
+        del C
+
+    el = timed_steps(run, steps, warmup, barrier)
+    units = nz[0] * steps
+    if dist is not None:
+        import torch
+        dev = f"cuda:{os.environ.get('LOCAL_RANK', '0')}" if comm is not None else "cpu"
+        t = torch.tensor([el, float(units)], dtype=torch.float64, device=dev)
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        el, units = float(tm[0].item()), int(t[1].item())
+    out = {"workload": "100^3 Moore torus thinned to 3 e/n (seed [42;32]), C = A^3 * A, u32 (config C4)",
+           "n_gpus": world, "rows": [lo, hi], "cuts": cuts if world <= 16 else None,
+           "ms_per_step": round(el / steps * 1e3, 4), "gnnz_per_s": round(units / el / 1e9, 4)}
+    # the blocks assembled over RCCL (every rank), checked against the golden digests on rank 0
+    par = None
+    if comm is not None:  # RCCL (also at world size 1 under SLAT_FORCE_DIST)
+        C = P.matmul_rowblock(lo, hi, A, 0)
+        comm.allgather_rows(C)  # warm-up (RCCL connection setup)
+        dist.barrier()
+        tg = time.perf_counter()
+        full = comm.allgather_rows(C)
+        dist.barrier()
+        out["gather_ms"] = round((time.perf_counter() - tg) * 1e3, 3)
+        if rank == 0:
+            par = parity(full, side, power)
+        del full, C
+    elif world == 1:
+        C = P.matmul_rowblock(0, n, A, 0)
+        par = parity(C, side, power)
+        del C
+    out["parity"] = par
+    # the whole product alone on rank 0's GPU (the strong-scaling anchor of the same run)
+    if dist is not None:
+        dist.barrier()
+    if rank == 0:
+        if world == 1:
+            single = el / steps * 1e3
+        else:
+            def one():
+                C1 = P.matmul_rowblock(0, n, A, 0)
+                del C1
+            single = timed_steps(one, max(5, min(steps, 20)), 3, ctx.sync) / max(5, min(steps, 20)) * 1e3
+        out["single_gpu_ms"] = round(single, 4)
+        out["speedup"] = round(single / (el / steps * 1e3), 3)
+    if dist is not None:
+        dist.barrier()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,16 +212,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=50, help="untimed steps; the GPU needs ~10 ms of load to clock up")
     ap.add_argument("--side", type=int, default=30)
     ap.add_argument("--power", type=int, default=7, help="C = A^(power-1) * A")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
-                    help="N > 1 default: strong (config C4 split over the ranks); weak = one torus per rank")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak (default): the headline workload on every rank; strong: the C4 leg is the value")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 strong-scaling leg")
+    ap.add_argument("--c4-steps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--timing-every", type=int, default=4,
                     help="record the per-kernel HIP events (roofline) on every k-th timed step; the event "
                          "records cost host time, so the other steps run without them")
-    ap.add_argument("--gather", action="store_true",
-                    help="N > 1: after the timed region, assemble C's row blocks on every rank (allgatherv over "
-                         "RCCL) and report its time as config.gather_ms")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,41 +244,30 @@ def main():
     coll_dev = f"cuda:{local}" if backend == "nccl" else "cpu"
 
     ctx = slat.Context(dev_index)
-    scaling = args.scaling or ("strong" if dist is not None else "weak")
+    comm = slat_dist.Comm(ctx) if (dist is not None and backend == "nccl") else None
     side, power = args.side, args.power
-    if scaling == "strong" and dist is not None and side == 30 and power == 7:
-        side, power = 100, 4  # config C4: 100^3 torus, C = A^3 * A split over the ranks
-    comm = None
-    if dist is not None and scaling == "strong" and backend == "nccl":
-        # rank 0 builds the operands; B (= A) and the left operand reach the others over RCCL
-        # (one broadcast per array, outside the timed region)
-        comm = slat_dist.Comm(ctx)
-        A, P = build_inputs(side, power, ctx) if rank == 0 else (None, None)
-        A = comm.bcast(A, slat.CsrMatrix)
-        P = comm.bcast(P, slat.CsrMatrix)
-    else:
-        A, P = build_inputs(side, power, ctx)
-    n = A.n
-    row_lo, row_hi = 0, n
-    if scaling == "strong" and dist is not None:
-        # flops-balanced 1-D row blocks of the left operand, cut on the device
-        cuts = slat_dist.device_cuts(P, A, world)
-        row_lo, row_hi = cuts[rank], cuts[rank + 1]
-
-    def step(flags=0):
-        C = P.matmul_rowblock(row_lo, row_hi, A, flags)
-        nz = C.nnz()
-        del C
-        return nz
-
-    for _ in range(args.warmup):
-        step()
 
     def barrier():
         if dist is not None:
             dist.barrier()
         ctx.sync()
 
+    c4 = None
+    if args.scaling == "strong" and not args.no_c4:
+        c4 = c4_leg(ctx, dist, comm, rank, world, args.steps, args.warmup)
+
+    # the headline workload (weak scaling: every rank its own torus, the block-diagonal matrix)
+    A, P = build_inputs(side, power, ctx)
+    n = A.n
+
+    def step(flags=0):
+        C = P.matmul(A) if not flags else P.matmul_rowblock(0, n, A, flags)
+        nz = C.nnz()
+        del C
+        return nz
+
+    for _ in range(args.warmup):
+        step()
     barrier()
     sym, scan, num, tot, abl = [], [], [], [], []
     t0 = time.perf_counter()
@@ -188,93 +295,67 @@ def main():
         u = torch.tensor([units], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         units = int(u.item())
-
     value = units / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
-
-    single_ms = None
-    if dist is not None and scaling == "strong":
-        # the same product on one GPU (rank 0 alone), for the strong-scaling speedup
-        dist.barrier()
-        if rank == 0:
-            k = max(5, min(args.steps, 20))
-            for _ in range(3):
-                P.matmul_rowblock(0, n, A, 0)
-            ctx.sync()
-            ts = time.perf_counter()
-            for _ in range(k):
-                C1 = P.matmul_rowblock(0, n, A, 0)
-                del C1
-            ctx.sync()
-            single_ms = (time.perf_counter() - ts) / k * 1e3
-        dist.barrier()
-
-    gather_ms, gather_nnz = None, None
-    if dist is not None and args.gather:
-        # not part of the SpGEMM metric: C row blocks stay distributed for the next step (§8(e))
+    # one output of the timed workload against the golden digests (outside the timed region)
+    par = parity(P.matmul(A), side, power) if rank == 0 else None
+    if dist is not None:
         import torch
-        C = P.matmul_rowblock(row_lo, row_hi, A, 0)
-        if comm is not None:
-            # device-resident allgatherv over RCCL (libslat): u32 columns, native-width values
-            comm.allgather_rows(C)  # warm-up (RCCL connection setup)
-            dist.barrier()
-            tg = time.perf_counter()
-            full = comm.allgather_rows(C)
-            dist.barrier()
-            gather_ms = (time.perf_counter() - tg) * 1e3
-            gather_nnz = full.nnz()
-            del full
-        else:  # CPU rehearsal (gloo): the host restatement of the assembly
-            hc = C.host()
-            dist.barrier()
-            tg = time.perf_counter()
-            slat_dist.gather_blocks(hc.row_ptr, hc.col_idx, hc.values, device=torch.device(coll_dev))
-            dist.barrier()
-            gather_ms = (time.perf_counter() - tg) * 1e3
-            gather_nnz = None
-        del C
+        ok = torch.tensor([0 if par is False else 1], dtype=torch.int32, device=coll_dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    nnz_a = P.nnz()
+    del P
 
-    if rank == 0:
-        nnz_a = P.nnz() if row_hi - row_lo == n else int(P.row_ptr[row_hi] - P.row_ptr[row_lo])
-        alg = algorithmic_bytes(nnz_a, A.nnz(), nnz_c, row_hi - row_lo, 4)
-        num_ms = float(np.mean(num))
-        achieved = alg / (max(num_ms, 1e-6) * 1e-3) / 1e9
-        pmc = load_pmc(f"torus{side}_a{power}")
-        traffic = pmc.get("numeric_bytes_per_launch") if pmc else None
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "kernel": "k_numeric", "algorithmic_bytes": alg, "timed_steps": len(num),
-                    "kernel_ms": {"symbolic": round(float(np.mean(sym)), 4), "scan": round(float(np.mean(scan)), 4),
-                                  "numeric": round(num_ms, 4), "device_total": round(float(np.mean(tot)), 4)},
-                    "pipeline_frac": round(alg / (max(float(np.mean(tot)), 1e-6) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
-        cpu = None
-        if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(side, power, args.cpu_seconds)
-        workload = f"{side}^3 Moore torus thinned to 3 e/n (seed [42;32]), C = A^{power - 1} * A, u32 saturating"
-        out = {
-            "metric": "GNNZ/s (output nnz/s) for A×A on 30³ Moore torus, 1/2/4/8 GPUs",
-            "value": round(value, 4), "unit": "GNNZ/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": scaling,
-            "vs_baseline": round(value / README_CSR_PAR_A7_GNNZ, 2) if (side, power) == (30, 7) else None,
-            "dtype": "u32", "data": "synthetic (reference generator: ChaCha12 StdRng seed [42;32])",
-            "config": {"workload": workload, "nnz_c": nnz_c, "n": n, "rows": [row_lo, row_hi],
-                       "partition": "block-diagonal, one torus per rank" if scaling == "weak" else "flops-balanced row blocks",
-                       "capacity": stats["capacity"], "mode": stats["mode"], "window_words": stats["window_words"],
-                       **({"ablated_ms": round(float(np.mean(abl)), 4)} if os.environ.get("SLAT_ABLATE") else {}),
-                       **({"gather_ms": round(gather_ms, 3)} if gather_ms is not None else {}),
-                       **({"gather_nnz": gather_nnz} if gather_nnz is not None else {}),
-                       **({"single_gpu_ms": round(single_ms, 4), "strong_speedup": round(single_ms / ms_per_step, 3)}
-                          if single_ms is not None else {})},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), flush=True)
+    if c4 is None and not args.no_c4:
+        c4 = c4_leg(ctx, dist, comm, rank, world, args.c4_steps, 3)
+
     if comm is not None:
         comm.close()
+    if rank == 0:
+        emit(args, world, side, power, n, nnz_a, A.nnz(), nnz_c, value, ms_per_step, stats, sym, scan, num, tot, abl, par, c4)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def emit(args, world, side, power, n, nnz_a, nnz_b, nnz_c, value, ms_per_step, stats, sym, scan, num, tot, abl, par, c4):
+    alg = algorithmic_bytes(nnz_a, nnz_b, nnz_c, n, 4)
+    num_ms = float(np.mean(num))
+    achieved = alg / (max(num_ms, 1e-6) * 1e-3) / 1e9
+    pmc = load_pmc(f"torus{side}_a{power}")
+    traffic = pmc.get("numeric_bytes_per_launch") if pmc else None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": "k_numeric", "algorithmic_bytes": alg, "timed_steps": len(num),
+                "kernel_ms": {"symbolic": round(float(np.mean(sym)), 4), "scan": round(float(np.mean(scan)), 4),
+                              "numeric": round(num_ms, 4), "device_total": round(float(np.mean(tot)), 4)},
+                "pipeline_frac": round(alg / (max(float(np.mean(tot)), 1e-6) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    cpu = None
+    if not args.no_cpu and world == 1:
+        cpu = cpu_baseline(side, power, args.cpu_seconds)
+    workload = f"{side}^3 Moore torus thinned to 3 e/n (seed [42;32]), C = A^{power - 1} * A, u32 saturating"
+    strong = args.scaling == "strong" and c4 is not None
+    out = {
+        "metric": ("GNNZ/s (output nnz/s) for A^3×A on 100³ Moore torus (config C4), 1/2/4/8 GPUs" if strong
+                   else "GNNZ/s (output nnz/s) for A×A on 30³ Moore torus, 1/2/4/8 GPUs"),
+        "value": round(c4["gnnz_per_s"] if strong else value, 4), "unit": "GNNZ/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(c4["ms_per_step"] if strong else ms_per_step, 4), "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
+        # the reference's published CSR-par A^7 rate (README.md:46, unstated hardware)
+        "vs_baseline": round(value / README_CSR_PAR_A7_GNNZ, 2) if (not strong and (side, power) == (30, 7)) else None,
+        "parity": c4["parity"] if strong else par,
+        "dtype": "u32", "data": "synthetic (reference generator: ChaCha12 StdRng seed [42;32])",
+        "config": {"workload": workload, "nnz_c_per_rank": nnz_c, "n": n,
+                   "partition": "one torus per rank (block-diagonal), no data-path collective",
+                   "capacity": stats["capacity"], "mode": stats["mode"], "window_words": stats["window_words"],
+                   **({"ablated_ms": round(float(np.mean(abl)), 4)} if os.environ.get("SLAT_ABLATE") else {}),
+                   **({"c4": c4} if c4 is not None else {}),
+                   **({"c4_single_gpu_ms": c4.get("single_gpu_ms")} if c4 is not None else {})},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

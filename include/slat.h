@@ -231,6 +231,10 @@ slat_status slat_bcast_csr(slat_ctx *ctx, slat_comm *comm, slat_csr *m, int root
 /* Allgatherv of the ranks' C row blocks, in rank order, into a new library-owned matrix `full` on every
  * rank: row_ptr rebased on the device; payload nnz * (4 + value bytes) + rows * 8. */
 slat_status slat_allgather_rows(slat_ctx *ctx, slat_comm *comm, const slat_csr_view *block, slat_csr *full);
+/* The same assembly of row blocks that all live on this context's device (not collective): blocks
+ * [0, nblocks) stacked in order into a new library-owned matrix, each block's row_ptr taken relative
+ * to its first entry (views into a larger matrix allowed), row_ptr rebased on the device. */
+slat_status slat_concat_rows(slat_ctx *ctx, const slat_csr_view *blocks, uint32_t nblocks, slat_csr *full);
 
 /* --- the reference's SpGEMM consumers, device-resident --------------
  * Square matrices (n_rows == n_cols) for the iterated drivers; host views are staged to the device.

@@ -24,7 +24,9 @@
     a += b; d ^= a; d = ROTL(d, 8);                                                               \
     c += d; b ^= c; b = ROTL(b, 7);
 
-void orc_chacha12_block(const uint32_t key[8], uint64_t counter, uint32_t out[16]) {
+/* the ChaCha block function with `double_rounds` double rounds (ChaCha12: 6; ChaCha20: 10, which the
+ * tests use to check the core against the RFC 8439 zero-key keystream) */
+void orc_chacha_block(const uint32_t key[8], uint64_t counter, int double_rounds, uint32_t out[16]) {
     uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
     for (int i = 0; i < 8; ++i) s[4 + i] = key[i];
     s[12] = (uint32_t)counter;
@@ -33,7 +35,7 @@ void orc_chacha12_block(const uint32_t key[8], uint64_t counter, uint32_t out[16
     s[15] = 0;
     uint32_t x[16];
     memcpy(x, s, sizeof x);
-    for (int r = 0; r < 6; ++r) { /* 12 rounds = 6 double rounds */
+    for (int r = 0; r < double_rounds; ++r) {
         QR(x[0], x[4], x[8], x[12]);
         QR(x[1], x[5], x[9], x[13]);
         QR(x[2], x[6], x[10], x[14]);
@@ -44,6 +46,10 @@ void orc_chacha12_block(const uint32_t key[8], uint64_t counter, uint32_t out[16
         QR(x[3], x[4], x[9], x[14]);
     }
     for (int i = 0; i < 16; ++i) out[i] = x[i] + s[i];
+}
+
+void orc_chacha12_block(const uint32_t key[8], uint64_t counter, uint32_t out[16]) {
+    orc_chacha_block(key, counter, 6, out); /* 12 rounds = 6 double rounds */
 }
 
 void orc_rng_seed(orc_rng *r, const uint8_t seed[32]) {

@@ -72,6 +72,7 @@ uint32_t orc_rng_range_u32(orc_rng *r, uint32_t lo, uint32_t hi);
 double orc_rng_next_f64(orc_rng *r);
 int orc_random(orc_rng *rng, uint32_t n, uint64_t m, orc_csr *out);
 void orc_chacha12_block(const uint32_t key[8], uint64_t counter, uint32_t out[16]);
+void orc_chacha_block(const uint32_t key[8], uint64_t counter, int double_rounds, uint32_t out[16]);
 
 void orc_csr_free(orc_csr *m);
 int orc_from_coo(uint64_t n, uint64_t ntrip, const uint32_t *rows, const uint32_t *cols,

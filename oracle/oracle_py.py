@@ -56,6 +56,7 @@ def lib():
         L.orc_rng_range_u32.restype = C.c_uint32
         L.orc_random.argtypes = [P(_Rng), C.c_uint32, C.c_uint64, P(_Csr)]
         L.orc_chacha12_block.argtypes = [P(C.c_uint32), C.c_uint64, P(C.c_uint32)]
+        L.orc_chacha_block.argtypes = [P(C.c_uint32), C.c_uint64, C.c_int, P(C.c_uint32)]
         L.orc_csr_free.argtypes = [P(_Csr)]
         L.orc_from_coo.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                    P(_Csr)]
@@ -329,3 +330,12 @@ def torus_thinned(side: int, epn: float, rng: Rng) -> Csr:
     full = lattice([side, side, side], True)
     density = epn / (full.nnz / full.n)
     return thin(full, rng, density) if density < 1.0 else full
+
+
+def chacha_block(key_words, counter: int, double_rounds: int = 6):
+    """One ChaCha keystream block (16 u32 words) of the oracle's core: 6 double rounds = ChaCha12
+    (StdRng), 10 = ChaCha20 (the RFC 8439 vectors)."""
+    key = (C.c_uint32 * 8)(*key_words)
+    out = (C.c_uint32 * 16)()
+    lib().orc_chacha_block(key, counter, double_rounds, out)
+    return list(out)

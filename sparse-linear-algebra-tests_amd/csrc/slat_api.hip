@@ -23,19 +23,14 @@
 #include "slat.h"
 #include "slat_internal.hpp"
 #include "spgemm_kernels.hpp"
-#include "short_sort.hpp"
+#include "slat_launch.hpp"
+#include "slat_fat.hpp"  // the fat-row category (a workgroup and a dense LDS accumulator per row)
 
 using namespace slat;
 
 // max(B) for the CSR walk too (SLAT_NO_NARROW_CSR=1: the u64 slots of before, for A/B runs)
 static const bool kNarrowCsr = std::getenv("SLAT_NO_NARROW_CSR") == nullptr;
 static void dev_release_all(slat_ctx *ctx);
-// slat_fat.hip: the fat-row category (a workgroup and a dense LDS accumulator per row)
-namespace slat { struct FatArgs; }
-size_t slat_fat_ws(uint64_t n);
-slat_status slat_fat_select(slat_ctx *ctx, slat::Args &a, void *ws, slat::FatArgs *out);
-slat_status slat_fat_symbolic(slat_ctx *ctx, slat::FatArgs &f, const slat::Args &a, bool idx32);
-slat_status slat_fat_numeric(slat_ctx *ctx, slat::FatArgs &f, const slat::Args &a, int32_t dtype, bool f64any, bool idx32);
 
 extern "C" {
 
@@ -404,122 +399,6 @@ extern "C" slat_status slat_csr_max_row_nnz(slat_ctx *ctx, const slat_csr_view *
 // ---------------------------------------------------------------------------------------------
 // launch helpers (templated over semiring and traversal modes)
 // ---------------------------------------------------------------------------------------------
-template <typename Sem>
-static hipError_t launch_numeric(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
-    // wide launches: the hash category (a.hash == 1) and the window category (a.hash == 2) are
-    // instances of their own, so neither path's registers burden the other
-    if (a.hash == 4) {  // short rows sorted in registers (short_sort.hpp)
-        if constexpr (!Sem::kOrdered) hipLaunchKernelGGL((k_numeric_sort<Sem>), grid, dim3(kBlock), lds, s, a);
-        return hipGetLastError();
-    }
-    if (a.hash == 3) {  // batched short rows (integer semirings, ELL B)
-        if constexpr (std::is_same_v<Sem, SemU32>) {
-            if (idx32)
-                hipLaunchKernelGGL((k_numeric_short_u32<uint32_t>), grid, dim3(kBlock), lds, s, a);
-            else
-                hipLaunchKernelGGL((k_numeric_short_u32<uint64_t>), grid, dim3(kBlock), lds, s, a);
-        } else if constexpr (!Sem::kOrdered) {
-            if (idx32)
-                hipLaunchKernelGGL((k_numeric_short<Sem, uint32_t>), grid, dim3(kBlock), lds, s, a);
-            else
-                hipLaunchKernelGGL((k_numeric_short<Sem, uint64_t>), grid, dim3(kBlock), lds, s, a);
-        }
-        return hipGetLastError();
-    }
-    if (a.hash == 1) {
-        if (idx32 && ell)
-            hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true, 1>), grid, dim3(kBlock), lds, s, a);
-        else if (idx32)
-            hipLaunchKernelGGL((k_numeric<Sem, uint32_t, false, 1>), grid, dim3(kBlock), lds, s, a);
-        else if (ell)
-            hipLaunchKernelGGL((k_numeric<Sem, uint64_t, true, 1>), grid, dim3(kBlock), lds, s, a);
-        else
-            hipLaunchKernelGGL((k_numeric<Sem, uint64_t, false, 1>), grid, dim3(kBlock), lds, s, a);
-        return hipGetLastError();
-    }
-    if (a.hash == 2) {
-        if (idx32 && ell)
-            hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true, 2>), grid, dim3(kBlock), lds, s, a);
-        else if (idx32)
-            hipLaunchKernelGGL((k_numeric<Sem, uint32_t, false, 2>), grid, dim3(kBlock), lds, s, a);
-        else if (ell)
-            hipLaunchKernelGGL((k_numeric<Sem, uint64_t, true, 2>), grid, dim3(kBlock), lds, s, a);
-        else
-            hipLaunchKernelGGL((k_numeric<Sem, uint64_t, false, 2>), grid, dim3(kBlock), lds, s, a);
-        return hipGetLastError();
-    }
-    if (idx32 && ell)
-        hipLaunchKernelGGL((k_numeric<Sem, uint32_t, true>), grid, dim3(kBlock), lds, s, a);
-    else if (idx32)
-        hipLaunchKernelGGL((k_numeric<Sem, uint32_t, false>), grid, dim3(kBlock), lds, s, a);
-    else if (ell)
-        hipLaunchKernelGGL((k_numeric<Sem, uint64_t, true>), grid, dim3(kBlock), lds, s, a);
-    else
-        hipLaunchKernelGGL((k_numeric<Sem, uint64_t, false>), grid, dim3(kBlock), lds, s, a);
-    return hipGetLastError();
-}
-
-// resident blocks per CU of the numeric kernel instance (its grid is sized to that: the product
-// record in the workspace is indexed by resident wave)
-template <typename Sem>
-static int numeric_blocks_per_cu(bool idx32, bool ell, int mode, size_t lds) {
-    // cached per (instance, LDS size): the query costs microseconds of host time per call
-    static thread_local int cache_nb[32] = {};
-    static thread_local size_t cache_lds[32] = {};
-    const int ci = (idx32 ? 1 : 0) | (ell ? 2 : 0) | (mode << 2);
-    if (cache_lds[ci] == lds && cache_nb[ci] > 0) return cache_nb[ci];
-    int nb = 0;
-    hipError_t e;
-    auto occ = [&](auto kern) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kBlock, lds); };
-    if (mode == 4) {
-        if constexpr (!Sem::kOrdered)
-            e = occ(k_numeric_sort<Sem>);
-        else
-            e = hipErrorInvalidValue;
-    } else if (mode == 3) {
-        if constexpr (std::is_same_v<Sem, SemU32>)
-            e = idx32 ? occ(k_numeric_short_u32<uint32_t>) : occ(k_numeric_short_u32<uint64_t>);
-        else if constexpr (!Sem::kOrdered)
-            e = idx32 ? occ(k_numeric_short<Sem, uint32_t>) : occ(k_numeric_short<Sem, uint64_t>);
-        else
-            e = hipErrorInvalidValue;
-    } else if (mode == 1)
-        e = idx32 ? (ell ? occ(k_numeric<Sem, uint32_t, true, 1>) : occ(k_numeric<Sem, uint32_t, false, 1>))
-                  : (ell ? occ(k_numeric<Sem, uint64_t, true, 1>) : occ(k_numeric<Sem, uint64_t, false, 1>));
-    else if (mode == 2)
-        e = idx32 ? (ell ? occ(k_numeric<Sem, uint32_t, true, 2>) : occ(k_numeric<Sem, uint32_t, false, 2>))
-                  : (ell ? occ(k_numeric<Sem, uint64_t, true, 2>) : occ(k_numeric<Sem, uint64_t, false, 2>));
-    else
-        e = idx32 ? (ell ? occ(k_numeric<Sem, uint32_t, true>) : occ(k_numeric<Sem, uint32_t, false>))
-                  : (ell ? occ(k_numeric<Sem, uint64_t, true>) : occ(k_numeric<Sem, uint64_t, false>));
-    nb = (e == hipSuccess && nb > 0) ? nb : 1;
-    cache_lds[ci] = lds;
-    cache_nb[ci] = nb;
-    return nb;
-}
-
-static void launch_symbolic(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
-    if (a.hash == 1 || a.hash == 2) {
-        auto go = [&](auto kern) { kern<<<grid, dim3(kBlock), lds, s>>>(a); };
-        if (a.hash == 1) {
-            if (idx32) ell ? go(k_symbolic<uint32_t, true, 1>) : go(k_symbolic<uint32_t, false, 1>);
-            else ell ? go(k_symbolic<uint64_t, true, 1>) : go(k_symbolic<uint64_t, false, 1>);
-        } else {
-            if (idx32) ell ? go(k_symbolic<uint32_t, true, 2>) : go(k_symbolic<uint32_t, false, 2>);
-            else ell ? go(k_symbolic<uint64_t, true, 2>) : go(k_symbolic<uint64_t, false, 2>);
-        }
-        return;
-    }
-    if (idx32 && ell)
-        hipLaunchKernelGGL((k_symbolic<uint32_t, true>), grid, dim3(kBlock), lds, s, a);
-    else if (idx32)
-        hipLaunchKernelGGL((k_symbolic<uint32_t, false>), grid, dim3(kBlock), lds, s, a);
-    else if (ell)
-        hipLaunchKernelGGL((k_symbolic<uint64_t, true>), grid, dim3(kBlock), lds, s, a);
-    else
-        hipLaunchKernelGGL((k_symbolic<uint64_t, false>), grid, dim3(kBlock), lds, s, a);
-}
-
 // blocks of k_build_ell (each stores one B-value partial for k_scan_rows when u32)
 static uint32_t build_ell_blocks(const slat_csr_view *B, uint32_t wq) {
     return (uint32_t)std::max<uint64_t>(std::min<uint64_t>((B->n_rows * wq + kBlock - 1) / kBlock, 4096), 1);
@@ -717,7 +596,21 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     uint64_t maxrow_b = B->max_row_nnz;
     if (maxrow_b == 0 && (st = slat_csr_max_row_nnz(ctx, B, &maxrow_b))) return st;
-    const uint64_t a_nnz_block = A->nnz;  // upper bound for the block too
+    // A entries of the row block (C's capacity bound): the whole A's nnz, then rows x A's max row
+    // when known (no sync); a block whose bound is still large reads its two row_ptr words (one
+    // small round trip, against a call that takes milliseconds at that size)
+    uint64_t a_nnz_block = A->nnz;
+    if (n < A->n_rows) {
+        if (A->max_row_nnz) a_nnz_block = std::min<uint64_t>(a_nnz_block, n * A->max_row_nnz);
+        if ((unsigned __int128)a_nnz_block * maxrow_b * (4 + vs) > (256ull << 20)) {
+            SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, A->row_ptr + row_begin, 8, hipMemcpyDeviceToHost, ctx->stream));
+            SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards + 1, A->row_ptr + row_end, 8, hipMemcpyDeviceToHost, ctx->stream));
+            SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (ctx->h_shards[1] < ctx->h_shards[0] || ctx->h_shards[1] - ctx->h_shards[0] > A->nnz)
+                return fail(ctx, SLAT_EINVAL, "A.row_ptr is not monotonic over the row block");
+            a_nnz_block = ctx->h_shards[1] - ctx->h_shards[0];
+        }
+    }
 
     Args a = {};
     a.a_rp = A->row_ptr + row_begin;
@@ -768,36 +661,28 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // symbolic batches for every value type (it never reads values); numeric for the integer ones
     const bool sym_batched = hash && ell && !std::getenv("SLAT_NO_BATCH");
     const bool batched = sym_batched && (dt != SLAT_F64 || f64any);
-    // experiment (SLAT_SORT_SHORT=1): the batched short rows sorted in registers (short_sort.hpp)
-    // instead of LDS hash tables. Measured on C4 (100^3, A^3 * A): symbolic 1.06 ms vs 0.52 ms
-    // (the row-bound kernel + k_symbolic_short at the time), numeric 1.58 + 0.41 ms (rows past 64 groups in the window
-    // launch) vs 1.47 ms: one sort of 256 slots serves ~2 C4 rows against ~4-8 rows per hash
-    // table, so the hash category stays the default
-    static const bool kSortShort = std::getenv("SLAT_SORT_SHORT") != nullptr;
-    const bool sorted = sym_batched && kSortShort;
     if (sym_batched) {
         uint32_t cb = 1;
         while (cb < 64 && ((ncols - 1) >> cb)) ++cb;
         a.cbits = cb <= 25 ? cb : 0;
     }
     const size_t hash_lds =
-        (size_t)wpb * (dt == SLAT_U32     ? (!batched ? hash_bytes<SemU32>() : sorted ? sort_num_bytes<SemU32>() : short_bytes<SemU32>())
-                       : dt == SLAT_SAT64 ? (!batched ? hash_bytes<SemSat64>() : sorted ? sort_num_bytes<SemSat64>() : short_bytes<SemSat64>())
-                       : f64any ? (!batched ? hash_bytes<SemF64Any>() : sorted ? sort_num_bytes<SemF64Any>() : short_bytes<SemF64Any>())
+        (size_t)wpb * (dt == SLAT_U32     ? (!batched ? hash_bytes<SemU32>() : short_bytes<SemU32>())
+                       : dt == SLAT_SAT64 ? (!batched ? hash_bytes<SemSat64>() : short_bytes<SemSat64>())
+                       : f64any ? (!batched ? hash_bytes<SemF64Any>() : short_bytes<SemF64Any>())
                                 : hash_bytes<SemF64>());
     if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
     const size_t sym_lds = (size_t)wpb * asym.ww * 4, sym_hash_lds = (size_t)wpb * kSymHashT * 4;
     const uint64_t row_blocks = (n + wpb - 1) / wpb;
     const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * 16)));
+    const int sem = dt == SLAT_U32 ? kSemU32 : dt == SLAT_SAT64 ? kSemSat64 : f64any ? kSemF64Any : kSemF64;
+    const int hash_mode = batched ? 3 : 1;  // numeric instance of the short rows of a wide launch
     auto num_grid = [&](int mode, size_t lds) {
-        const int nbpc = dt == SLAT_U32     ? numeric_blocks_per_cu<SemU32>(idx32, ell, mode, lds)
-                         : dt == SLAT_SAT64 ? numeric_blocks_per_cu<SemSat64>(idx32, ell, mode, lds)
-                         : f64any           ? numeric_blocks_per_cu<SemF64Any>(idx32, ell, mode, lds)
-                                            : numeric_blocks_per_cu<SemF64>(idx32, ell, mode, lds);
+        const int nbpc = slat_numeric_blocks_per_cu(sem, mode, idx32, ell, lds);
         return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc)));
     };
     const dim3 grid = num_grid(hash ? 2 : 0, num_lds);
-    const dim3 hash_grid = hash ? num_grid(batched ? (sorted ? 4 : 3) : 1, hash_lds) : dim3(1);
+    const dim3 hash_grid = hash ? num_grid(hash_mode, hash_lds) : dim3(1);
     const bool progress = g_progress.load(std::memory_order_relaxed) != 0;
     const bool timing = (flags & SLAT_FLAG_TIMING) || progress;
 
@@ -819,10 +704,9 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
-    // batched wide launches: row product bounds u32[n] | symbolic / numeric window-row lists u32[n]
-    // | their counters
-    const size_t o_rb = o_smask + smask_b, rb_b = sym_batched ? up256(n * 4) : 0;
-    const size_t o_l1 = o_rb + rb_b, o_l2 = o_l1 + rb_b, o_lc = o_l2 + rb_b, lc_b = sym_batched ? 256 : 0;
+    // batched wide launches: symbolic / numeric window-row lists u32[n] | their counters
+    const size_t list_b = sym_batched ? up256(n * 4) : 0;
+    const size_t o_l1 = o_smask + smask_b, o_l2 = o_l1 + list_b, o_lc = o_l2 + list_b, lc_b = sym_batched ? 256 : 0;
     // fat rows (MAGNUS's dense-accumulation category) once a row can reach kFat products:
     // max row of A x max row of B (A's max row unknown: when B has long rows)
     static const bool kNoFat = std::getenv("SLAT_NO_FAT") != nullptr;
@@ -870,7 +754,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         return e ? std::strtoull(e, nullptr, 10) : (4ull << 30);
     }();
     const unsigned __int128 budget = std::min<unsigned __int128>(ctx->free_b / 4, kBoundBytes);
-    const bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
+    bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
     // C's arrays in three pieces: row_ptr, then col_idx and values sized by the bound; after the
     // call both are trimmed to nnz(C) and their tails go back to the context's cache
     SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&C->row_ptr, (n + 1) * 8, s));
@@ -879,15 +763,32 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         C->capacity = (uint64_t)std::max<unsigned __int128>(bound128, 1);
         if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
             slat_dev_alloc(ctx, &C->values, C->capacity * vs, s) != hipSuccess) {
-            slat_csr_free(ctx, C);
-            return fail(ctx, SLAT_EOOM, "C allocation failed");
+            // the bound does not fit (or the cache is fragmented): the exact-size path instead
+            (void)hipGetLastError();
+            if (C->col_idx) slat_dev_free(ctx, C->col_idx, s);
+            C->col_idx = nullptr;
+            C->capacity = 0;
+            exact = true;
         }
     }
     a.c_rp = C->row_ptr;
-
+    // C's pieces are live from here: every error return frees them
+    auto failc = [&](slat_status e) {
+        (void)hipStreamSynchronize(s);
+        slat_csr_free(ctx, C);
+        return e;
+    };
+#define SLAT_HIPC(expr)                                                                            \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);                          \
+            return failc(SLAT_EHIP);                                                               \
+        }                                                                                          \
+    } while (0)
 
     hc.mark(0);
-    if (a.stats || SLAT_PHASES) SLAT_HIP(ctx, hipMemsetAsync(a.shards, 0, shards_b, s));
+    if (a.stats || SLAT_PHASES) SLAT_HIPC(hipMemsetAsync(a.shards, 0, shards_b, s));
     asym.counts = a.counts;
     asym.shards = a.shards;
     asym.c_rp = a.c_rp;
@@ -907,17 +808,17 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
         else
             be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
-        SLAT_HIP(ctx, be);
+        SLAT_HIPC(be);
     } else if (a.b_vmax && B->nnz) {
         const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
         hipLaunchKernelGGL(k_bvmax, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz, ctx->d_vmax,
                            a.epoch);
-        SLAT_HIP(ctx, hipGetLastError());
+        SLAT_HIPC(hipGetLastError());
     }
-    alignas(16) uint8_t fat_store[1024];
-    slat::FatArgs *fa = (slat::FatArgs *)fat_store;
+    slat::FatArgs fat_args = {};
+    slat::FatArgs *fa = &fat_args;
     if (fat) {
-        if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return st;
+        if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return failc(st);
         asym.fr_mark = a.fr_mark;
     }
     if (ablate & 7u) {
@@ -926,58 +827,43 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         abl.ablate = ablate;
         abl.counts = (uint64_t *)(ws + o_abl);
         abl.c_rp = abl.counts;  // row_ptr[0] store lands in scratch too
-        SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
-        launch_symbolic(idx32, ell, sym_grid, sym_lds, s, abl);
-        SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
+        SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
+        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, abl));
+        SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
     }
-    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[0], s));
-    if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return st;
+    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[0], s));
+    if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return failc(st);
     if (sym_batched) {
         // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
         // row's products per tile, listing the rest), then the listed rows by windows
         unsigned int *lc = (unsigned int *)(ws + o_lc);
-        SLAT_HIP(ctx, hipMemsetAsync(lc, 0, lc_b, s));
-        uint32_t *rb = (uint32_t *)(ws + o_rb);
+        SLAT_HIPC(hipMemsetAsync(lc, 0, lc_b, s));
         Args h1 = asym, h2 = asym;
-        h1.rbound = rb;
         h1.cbits = a.cbits;
         h1.list = h2.list = (uint32_t *)(ws + o_l1);
         h1.list_cnt = h2.list_cnt = lc;
-        h2.hash = 2;
         const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kWave - 1) / kWave / wpb + 1, ctx->cu_count * 16ull)));
-        if (sorted)  // also writes the rows' ELL group counts into rb for the numeric pass
-            hipLaunchKernelGGL(k_symbolic_sort, g1, dim3(kBlock), wpb * sort_sym_bytes(), s, h1);
-        else if (idx32)
-            hipLaunchKernelGGL(k_symbolic_short<uint32_t>, g1, dim3(kBlock), wpb * sym_short_bytes(), s, h1);
-        else
-            hipLaunchKernelGGL(k_symbolic_short<uint64_t>, g1, dim3(kBlock), wpb * sym_short_bytes(), s, h1);
-        SLAT_HIP(ctx, hipGetLastError());
-        launch_symbolic(idx32, ell, sym_grid, sym_lds, s, h2);
+        SLAT_HIPC(slat_launch_symbolic_short(idx32, g1, wpb * sym_short_bytes(), s, h1));
+        SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
         a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
-        a.rbound = rb;                      // k_numeric_sort's batch formation
         a.list_cnt = lc + 16;
     } else if (hash) {
-        Args h1 = asym, h2 = asym;
-        h1.hash = 1;
-        h2.hash = 2;
-        launch_symbolic(idx32, ell, sym_grid, sym_hash_lds, s, h1);
-        SLAT_HIP(ctx, hipGetLastError());
-        launch_symbolic(idx32, ell, sym_grid, sym_lds, s, h2);
+        SLAT_HIPC(slat_launch_symbolic(1, idx32, ell, sym_grid, sym_hash_lds, s, asym));
+        SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, asym));
     } else {
-        launch_symbolic(idx32, ell, sym_grid, sym_lds, s, asym);
+        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
     }
-    SLAT_HIP(ctx, hipGetLastError());
-    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[1], s));
+    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
     // (u32 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
     const bool bpart = ell && dt == SLAT_U32;
     if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
                                bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
                                bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch)))
-        return st;
-    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+        return failc(st);
+    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
 
     if (exact) {
-        SLAT_HIP(ctx, hipStreamSynchronize(s));
+        SLAT_HIPC(hipStreamSynchronize(s));
         const uint64_t total = ctx->h_out[0];
         C->capacity = std::max<uint64_t>(total, 1);
         if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
@@ -985,46 +871,36 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             slat_csr_free(ctx, C);
             return fail(ctx, SLAT_EOOM, "C allocation failed");
         }
-        if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[2], s));
+        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
     }
     a.c_col = C->col_idx;
     a.c_val = C->values;
     hipError_t e;
-    auto launch_num = [&](const Args &x) -> hipError_t {
-        if (dt == SLAT_U32) return launch_numeric<SemU32>(idx32, ell, grid, num_lds, s, x);
-        if (dt == SLAT_SAT64) return launch_numeric<SemSat64>(idx32, ell, grid, num_lds, s, x);
-        if (f64any) return launch_numeric<SemF64Any>(idx32, ell, grid, num_lds, s, x);
-        return launch_numeric<SemF64>(idx32, ell, grid, num_lds, s, x);
-    };
+    const int win_mode = hash ? 2 : 0;  // numeric instance of the window rows
+    auto launch_num = [&](const Args &x) { return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x); };
     if (ablate & ~7u) {
         // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
         // the real numeric pass below overwrites everything it wrote
         Args abl = a;
         abl.ablate = ablate;
         abl.counts = (uint64_t *)(ws + o_abl);
-        SLAT_HIP(ctx, hipEventRecord(ctx->ev[4], s));
-        SLAT_HIP(ctx, launch_num(abl));
-        SLAT_HIP(ctx, hipEventRecord(ctx->ev[5], s));
+        SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
+        SLAT_HIPC(launch_num(abl));
+        SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
     }
     if (hash) {
         Args h1 = a;
-        h1.hash = batched ? (sorted ? 4 : 3) : 1;
-        a.hash = 2;
         if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
-        hipError_t he;
-        if (dt == SLAT_U32) he = launch_numeric<SemU32>(idx32, ell, hash_grid, hash_lds, s, h1);
-        else if (dt == SLAT_SAT64) he = launch_numeric<SemSat64>(idx32, ell, hash_grid, hash_lds, s, h1);
-        else if (f64any) he = launch_numeric<SemF64Any>(idx32, ell, hash_grid, hash_lds, s, h1);
-        else he = launch_numeric<SemF64>(idx32, ell, hash_grid, hash_lds, s, h1);
-        SLAT_HIP(ctx, he);
+        SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
     }
-    SLAT_HIP(ctx, launch_num(a));
-    if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return st;
-    if (timing) SLAT_HIP(ctx, hipEventRecord(ctx->ev[3], s));
-    if (a.stats) SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
+    SLAT_HIPC(launch_num(a));
+    if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return failc(st);
+    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));
+    if (a.stats) SLAT_HIPC(hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                              hipMemcpyDeviceToHost, s));
     hc.mark(1);
-    SLAT_HIP(ctx, wait_stream(ctx, s));
+    SLAT_HIPC(wait_stream(ctx, s));
+#undef SLAT_HIPC
     hc.mark(2);
     if (SLAT_PHASES) {
         // diagnostic build: per-phase cycles of the numeric kernel, summed over waves

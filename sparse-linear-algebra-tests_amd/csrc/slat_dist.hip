@@ -177,6 +177,114 @@ extern "C" slat_status slat_rowblock_cuts(slat_ctx *ctx, const slat_csr_view *A,
     return SLAT_OK;
 }
 
+// RCCL calls whose failure must not strand the other ranks: the first error is kept and the caller
+// still reaches ncclGroupEnd / the status agreement
+#define SLAT_NCCL_KEEP(ctx, st, expr)                                                                  \
+    do {                                                                                               \
+        ncclResult_t r_ = (expr);                                                                      \
+        if (r_ != ncclSuccess && (st) == SLAT_OK) {                                                    \
+            (ctx)->err = std::string(#expr) + ": " + ncclGetErrorString(r_);                           \
+            (st) = SLAT_EHIP;                                                                          \
+        }                                                                                              \
+    } while (0)
+
+namespace {
+
+// every rank's status agreed on (the max over ranks) before data moves: a rank that failed to
+// allocate must not leave the others blocked inside broadcasts it never joins
+slat_status agree(slat_ctx *ctx, slat_comm *comm, slat_status mine) {
+    const hipStream_t s = ctx->stream;
+    uint32_t *w = nullptr;
+    if (slat_dev_alloc(ctx, (void **)&w, 8, s) != hipSuccess) {
+        // cannot even agree: report this rank's failure (the others see RCCL's own timeout)
+        return mine != SLAT_OK ? mine : fail(ctx, SLAT_EOOM, "status word allocation failed");
+    }
+    uint32_t v = (uint32_t)mine, got = 0;
+    slat_status st = SLAT_OK;
+    if (hipMemcpyAsync(w, &v, 4, hipMemcpyHostToDevice, s) != hipSuccess) st = SLAT_EHIP;
+    SLAT_NCCL_KEEP(ctx, st, ncclAllReduce(w, w + 1, 1, ncclUint32, ncclMax, comm->nc, s));
+    if (hipMemcpyAsync(&got, w + 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        st = SLAT_EHIP;
+    slat_dev_free(ctx, w, s);
+    if (st != SLAT_OK) return st;
+    if (got != SLAT_OK && mine == SLAT_OK) return fail(ctx, (slat_status)got, "another rank failed");
+    return (slat_status)got;
+}
+
+// The row-block assembly shared by slat_allgather_rows (blocks from every rank over RCCL) and
+// slat_concat_rows (blocks on this device): block r's rows land at row_off[r], its entries at
+// nnz_off[r]; its row ends are copied relative to its own first entry and rebased on the device.
+struct Assembly {
+    std::vector<uint64_t> row_off, nnz_off;
+    uint64_t maxrow = 0;
+    uint64_t *tab = nullptr;  // device: row_off [P + 1] | nnz_off [P + 1]
+};
+
+// offsets from every block's (rows, nnz, max row, dtype); C's arrays and the device offset table
+slat_status assembly_plan(slat_ctx *ctx, const uint64_t *meta, int P, int32_t dt, uint64_t n_cols, Assembly &a,
+                          slat_csr *full) {
+    a.row_off.assign(P + 1, 0);
+    a.nnz_off.assign(P + 1, 0);
+    for (int r = 0; r < P; ++r) {
+        if ((int32_t)meta[4 * r + 3] != dt) return fail(ctx, SLAT_EINVAL, "the row blocks differ in value type");
+        a.row_off[r + 1] = a.row_off[r] + meta[4 * r];
+        a.nnz_off[r + 1] = a.nnz_off[r] + meta[4 * r + 1];
+        a.maxrow = std::max(a.maxrow, meta[4 * r + 2]);
+    }
+    const hipStream_t s = ctx->stream;
+    std::memset(full, 0, sizeof *full);
+    if (alloc_joint(ctx, full, a.row_off[P], a.nnz_off[P], vsize(dt), s) != hipSuccess)
+        return fail(ctx, SLAT_EOOM, "assembled matrix allocation failed");
+    full->n_rows = a.row_off[P];
+    full->n_cols = n_cols;
+    full->nnz = a.nnz_off[P];
+    full->capacity = std::max<uint64_t>(a.nnz_off[P], 1);
+    full->dtype = dt;
+    full->max_row_nnz = a.maxrow;
+    full->device = ctx->device;
+    if (slat_dev_alloc(ctx, (void **)&a.tab, (size_t)(2 * P + 2) * 8, s) != hipSuccess) {
+        slat_csr_free(ctx, full);
+        return fail(ctx, SLAT_EOOM, "offset table allocation failed");
+    }
+    if (hipMemcpyAsync(a.tab, a.row_off.data(), (P + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(a.tab + P + 1, a.nnz_off.data(), (P + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess) {
+        slat_dev_free(ctx, a.tab, s);
+        a.tab = nullptr;
+        slat_csr_free(ctx, full);
+        return fail(ctx, SLAT_EHIP, "offset table upload failed");
+    }
+    return SLAT_OK;
+}
+
+// full.row_ptr[0] = 0 and block r's row ends + nnz_off[r], then the stream drained
+slat_status assembly_finish(slat_ctx *ctx, Assembly &a, slat_csr *full, int P) {
+    const hipStream_t s = ctx->stream;
+    hipLaunchKernelGGL(k_rebase, dim3(grid_for(ctx, std::max<uint64_t>(a.row_off[P], 1))), dim3(kB), 0, s, full->row_ptr,
+                       a.tab, a.tab + P + 1, P);
+    const hipError_t e = hipGetLastError();
+    slat_dev_free(ctx, a.tab, s);
+    a.tab = nullptr;
+    SLAT_HIP(ctx, e);
+    SLAT_HIP(ctx, hipStreamSynchronize(s));
+    return SLAT_OK;
+}
+
+// a block's row ends relative to its first entry: the view's own row_ptr + 1 when it starts at 0,
+// else a temporary (*tmp, freed by the caller) filled by k_rel_ends
+slat_status rel_ends(slat_ctx *ctx, const slat_csr_view *b, uint64_t first, const uint64_t **ends, uint64_t **tmp) {
+    *tmp = nullptr;
+    *ends = b->row_ptr + 1;
+    if (first == 0 || b->n_rows == 0) return SLAT_OK;
+    const hipStream_t s = ctx->stream;
+    if (slat_dev_alloc(ctx, (void **)tmp, b->n_rows * 8, s) != hipSuccess) return fail(ctx, SLAT_EOOM, "row-end scratch");
+    hipLaunchKernelGGL(k_rel_ends, dim3(grid_for(ctx, b->n_rows)), dim3(kB), 0, s, b->row_ptr, b->n_rows, first, *tmp);
+    SLAT_HIP(ctx, hipGetLastError());
+    *ends = *tmp;
+    return SLAT_OK;
+}
+
+}  // namespace
+
 extern "C" slat_status slat_bcast_csr(slat_ctx *ctx, slat_comm *comm, slat_csr *m, int root) {
     if (!ctx || !comm || !m || root < 0 || root >= comm->nranks) return SLAT_EINVAL;
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
@@ -185,114 +293,175 @@ extern "C" slat_status slat_bcast_csr(slat_ctx *ctx, slat_comm *comm, slat_csr *
     uint64_t meta[5] = {m->n_rows, m->n_cols, m->nnz, (uint64_t)m->dtype, m->max_row_nnz};
     uint64_t *dmeta = nullptr;
     SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&dmeta, sizeof meta, s));
-    SLAT_HIP(ctx, hipMemcpyAsync(dmeta, meta, sizeof meta, hipMemcpyHostToDevice, s));
-    SLAT_NCCL(ctx, ncclBroadcast(dmeta, dmeta, 5, ncclUint64, root, comm->nc, s));
-    SLAT_HIP(ctx, hipMemcpyAsync(meta, dmeta, sizeof meta, hipMemcpyDeviceToHost, s));
-    SLAT_HIP(ctx, hipStreamSynchronize(s));
+    slat_status st = SLAT_OK;
+    if (hipMemcpyAsync(dmeta, meta, sizeof meta, hipMemcpyHostToDevice, s) != hipSuccess) st = fail(ctx, SLAT_EHIP, "meta upload");
+    SLAT_NCCL_KEEP(ctx, st, ncclBroadcast(dmeta, dmeta, 5, ncclUint64, root, comm->nc, s));
+    if (hipMemcpyAsync(meta, dmeta, sizeof meta, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        if (st == SLAT_OK) st = fail(ctx, SLAT_EHIP, "meta read-back");
     slat_dev_free(ctx, dmeta, s);
+    if (st != SLAT_OK) return st;
     const int32_t dt = (int32_t)meta[3];
-    if (dt < SLAT_U32 || dt > SLAT_F64) return fail(ctx, SLAT_EINVAL, "broadcast matrix: bad dtype");
+    if (dt < SLAT_U32 || dt > SLAT_F64) return fail(ctx, SLAT_EINVAL, "broadcast matrix: bad dtype");  // on every rank
+    slat_status mine = SLAT_OK;
     if (comm->rank != root) {
         std::memset(m, 0, sizeof *m);
-        SLAT_HIP(ctx, alloc_joint(ctx, m, meta[0], meta[2], vsize(dt), s));
-        m->n_rows = meta[0];
-        m->n_cols = meta[1];
-        m->nnz = meta[2];
-        m->capacity = meta[2];
-        m->dtype = dt;
-        m->max_row_nnz = meta[4];
-        m->device = ctx->device;
+        if (alloc_joint(ctx, m, meta[0], meta[2], vsize(dt), s) != hipSuccess) {
+            std::memset(m, 0, sizeof *m);
+            mine = fail(ctx, SLAT_EOOM, "broadcast matrix allocation failed");
+        } else {
+            m->n_rows = meta[0];
+            m->n_cols = meta[1];
+            m->nnz = meta[2];
+            m->capacity = meta[2];
+            m->dtype = dt;
+            m->max_row_nnz = meta[4];
+            m->device = ctx->device;
+        }
     }
-    SLAT_NCCL(ctx, ncclGroupStart());
-    SLAT_NCCL(ctx, ncclBroadcast(m->row_ptr, m->row_ptr, m->n_rows + 1, ncclUint64, root, comm->nc, s));
-    if (m->nnz) {
-        SLAT_NCCL(ctx, ncclBroadcast(m->col_idx, m->col_idx, m->nnz, ncclUint32, root, comm->nc, s));
-        SLAT_NCCL(ctx, ncclBroadcast(m->values, m->values, m->nnz, value_type(dt), root, comm->nc, s));
+    if ((st = agree(ctx, comm, mine)) != SLAT_OK) {
+        if (comm->rank != root && m->row_ptr) slat_csr_free(ctx, m);
+        return st;
     }
-    SLAT_NCCL(ctx, ncclGroupEnd());
+    SLAT_NCCL_KEEP(ctx, st, ncclGroupStart());
+    SLAT_NCCL_KEEP(ctx, st, ncclBroadcast(m->row_ptr, m->row_ptr, meta[0] + 1, ncclUint64, root, comm->nc, s));
+    if (meta[2]) {
+        SLAT_NCCL_KEEP(ctx, st, ncclBroadcast(m->col_idx, m->col_idx, meta[2], ncclUint32, root, comm->nc, s));
+        SLAT_NCCL_KEEP(ctx, st, ncclBroadcast(m->values, m->values, meta[2], value_type(dt), root, comm->nc, s));
+    }
+    SLAT_NCCL_KEEP(ctx, st, ncclGroupEnd());
+    if (st != SLAT_OK) return st;
     SLAT_HIP(ctx, hipStreamSynchronize(s));
     return SLAT_OK;
 }
 
 extern "C" slat_status slat_allgather_rows(slat_ctx *ctx, slat_comm *comm, const slat_csr_view *block, slat_csr *full) {
     if (!ctx || !comm || !block || !full) return SLAT_EINVAL;
-    slat_status st;
-    if ((st = slat_check_view(ctx, block, "block"))) return st;
-    if (block->residency != SLAT_DEVICE) return fail(ctx, SLAT_EINVAL, "device views only");
+    std::memset(full, 0, sizeof *full);
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    // a malformed block is not returned on at once: every rank must reach the metadata gather, so
+    // the block travels as an invalid dtype and every rank refuses the assembly together
+    slat_status vst = slat_check_view(ctx, block, "block");
+    if (vst == SLAT_OK && block->residency != SLAT_DEVICE) vst = fail(ctx, SLAT_EINVAL, "device views only");
     const hipStream_t s = ctx->stream;
     const int P = comm->nranks;
-    const int32_t dt = block->dtype;
-    // every block's (rows, nnz, max row, dtype, first row_ptr entry); a block's row_ptr may be a view
-    // into a larger matrix (absolute offsets), so its entries are relative to row_ptr[0]
+    const int32_t dt = vst == SLAT_OK ? block->dtype : -1;
+    // every block's (rows, nnz, max row, dtype); a block's row_ptr may be a view into a larger matrix
+    // (absolute offsets), so its entries are taken relative to row_ptr[0]
     uint64_t first = 0;
-    if (block->n_rows) SLAT_HIP(ctx, hipMemcpyAsync(&first, block->row_ptr, 8, hipMemcpyDeviceToHost, s));
+    if (vst == SLAT_OK && block->n_rows) SLAT_HIP(ctx, hipMemcpyAsync(&first, block->row_ptr, 8, hipMemcpyDeviceToHost, s));
     SLAT_HIP(ctx, hipStreamSynchronize(s));
-    const uint64_t mine[4] = {block->n_rows, block->nnz, block->max_row_nnz, (uint64_t)dt};
+    const uint64_t mine[4] = {vst == SLAT_OK ? block->n_rows : 0, vst == SLAT_OK ? block->nnz : 0,
+                              vst == SLAT_OK ? block->max_row_nnz : 0, (uint64_t)(int64_t)dt};
     std::vector<uint64_t> all((size_t)4 * P);
     uint64_t *dm = nullptr;
     SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&dm, (size_t)(4 + 4 * P) * 8, s));
-    SLAT_HIP(ctx, hipMemcpyAsync(dm, mine, sizeof mine, hipMemcpyHostToDevice, s));
-    SLAT_NCCL(ctx, ncclAllGather(dm, dm + 4, 4, ncclUint64, comm->nc, s));
-    SLAT_HIP(ctx, hipMemcpyAsync(all.data(), dm + 4, all.size() * 8, hipMemcpyDeviceToHost, s));
-    SLAT_HIP(ctx, hipStreamSynchronize(s));
+    slat_status st = SLAT_OK;
+    if (hipMemcpyAsync(dm, mine, sizeof mine, hipMemcpyHostToDevice, s) != hipSuccess) st = fail(ctx, SLAT_EHIP, "meta upload");
+    SLAT_NCCL_KEEP(ctx, st, ncclAllGather(dm, dm + 4, 4, ncclUint64, comm->nc, s));
+    if ((hipMemcpyAsync(all.data(), dm + 4, all.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+         hipStreamSynchronize(s) != hipSuccess) && st == SLAT_OK)
+        st = fail(ctx, SLAT_EHIP, "meta read-back");
     slat_dev_free(ctx, dm, s);
-    std::vector<uint64_t> row_off(P + 1, 0), nnz_off(P + 1, 0);
-    uint64_t maxrow = 0;
-    for (int r = 0; r < P; ++r) {
-        if ((int32_t)all[4 * r + 3] != dt) return fail(ctx, SLAT_EINVAL, "ranks' blocks differ in value type");
-        row_off[r + 1] = row_off[r] + all[4 * r];
-        nnz_off[r + 1] = nnz_off[r] + all[4 * r + 1];
-        maxrow = std::max(maxrow, all[4 * r + 2]);
+    if (st != SLAT_OK) return st;
+    for (int r = 0; r < P; ++r)
+        if ((int32_t)all[4 * r + 3] < SLAT_U32 || (int32_t)all[4 * r + 3] > SLAT_F64)
+            return vst != SLAT_OK ? vst : fail(ctx, SLAT_EINVAL, "another rank's block is malformed");
+    // every allocation before the data moves, then one agreed status
+    Assembly a;
+    uint64_t *my_ends_tmp = nullptr;
+    const uint64_t *my_ends = nullptr;
+    slat_status mine_st = assembly_plan(ctx, all.data(), P, dt, block->n_cols, a, full);  // same verdict on every rank
+    if (mine_st == SLAT_OK) mine_st = rel_ends(ctx, block, first, &my_ends, &my_ends_tmp);
+    auto cleanup = [&]() {
+        if (my_ends_tmp) slat_dev_free(ctx, my_ends_tmp, s);
+        if (a.tab) slat_dev_free(ctx, a.tab, s);
+        a.tab = nullptr;
+    };
+    if ((st = agree(ctx, comm, mine_st)) != SLAT_OK) {
+        cleanup();
+        if (full->row_ptr) slat_csr_free(ctx, full);
+        return st;
     }
-    std::memset(full, 0, sizeof *full);
-    SLAT_HIP(ctx, alloc_joint(ctx, full, row_off[P], nnz_off[P], vsize(dt), s));
-    full->n_rows = row_off[P];
-    full->n_cols = block->n_cols;
-    full->nnz = nnz_off[P];
-    full->capacity = std::max<uint64_t>(nnz_off[P], 1);
-    full->dtype = dt;
-    full->max_row_nnz = maxrow;
-    full->device = ctx->device;
-    // the blocks' row ends (local, rebased below), columns and values: one broadcast per root and array
-    const bool me_rel = first == 0;
-    uint64_t *my_ends = nullptr;  // this block's row_ptr[1..] relative to its first entry
-    if (!me_rel && block->n_rows) {
-        SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&my_ends, block->n_rows * 8, s));
-        hipLaunchKernelGGL(k_rel_ends, dim3(grid_for(ctx, block->n_rows)), dim3(kB), 0, s, block->row_ptr, block->n_rows,
-                           first, my_ends);
-        SLAT_HIP(ctx, hipGetLastError());
-    }
+    // the blocks' row ends (relative, rebased below), columns and values: one broadcast per root and
+    // array, inside one group that is always closed
     const uint8_t *my_col = (const uint8_t *)block->col_idx + first * 4;
     const uint8_t *my_val = (const uint8_t *)block->values + first * vsize(dt);
-    SLAT_NCCL(ctx, ncclGroupStart());
-    for (int r = 0; r < P; ++r) {
+    SLAT_NCCL_KEEP(ctx, st, ncclGroupStart());
+    for (int r = 0; r < P && st == SLAT_OK; ++r) {
         const uint64_t rows = all[4 * r], nz = all[4 * r + 1];
         const bool me = r == comm->rank;
         if (rows)
-            SLAT_NCCL(ctx, ncclBroadcast(me ? (const void *)(me_rel ? block->row_ptr + 1 : my_ends) : nullptr,
-                                         full->row_ptr + 1 + row_off[r], rows, ncclUint64, r, comm->nc, s));
+            SLAT_NCCL_KEEP(ctx, st, ncclBroadcast(me ? (const void *)my_ends : nullptr, full->row_ptr + 1 + a.row_off[r],
+                                                  rows, ncclUint64, r, comm->nc, s));
         if (nz) {
-            SLAT_NCCL(ctx, ncclBroadcast(me ? (const void *)my_col : nullptr, full->col_idx + nnz_off[r], nz, ncclUint32,
-                                         r, comm->nc, s));
-            SLAT_NCCL(ctx, ncclBroadcast(me ? (const void *)my_val : nullptr,
-                                         (uint8_t *)full->values + nnz_off[r] * vsize(dt), nz, value_type(dt), r,
-                                         comm->nc, s));
+            SLAT_NCCL_KEEP(ctx, st, ncclBroadcast(me ? (const void *)my_col : nullptr, full->col_idx + a.nnz_off[r], nz,
+                                                  ncclUint32, r, comm->nc, s));
+            SLAT_NCCL_KEEP(ctx, st, ncclBroadcast(me ? (const void *)my_val : nullptr,
+                                                  (uint8_t *)full->values + a.nnz_off[r] * vsize(dt), nz, value_type(dt),
+                                                  r, comm->nc, s));
         }
     }
-    SLAT_NCCL(ctx, ncclGroupEnd());
-    // rebase: block r's (relative) row ends + nnz_off[r]
-    std::vector<uint64_t> add(P + 1, 0);
-    for (int r = 0; r < P; ++r) add[r] = nnz_off[r];
-    uint64_t *tab = nullptr;
-    SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&tab, (size_t)(2 * P + 2) * 8, s));
-    SLAT_HIP(ctx, hipMemcpyAsync(tab, row_off.data(), (P + 1) * 8, hipMemcpyHostToDevice, s));
-    SLAT_HIP(ctx, hipMemcpyAsync(tab + P + 1, add.data(), (P + 1) * 8, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_rebase, dim3(grid_for(ctx, std::max<uint64_t>(row_off[P], 1))), dim3(kB), 0, s, full->row_ptr,
-                       tab, tab + P + 1, P);
-    SLAT_HIP(ctx, hipGetLastError());
-    if (my_ends) slat_dev_free(ctx, my_ends, s);
-    slat_dev_free(ctx, tab, s);
+    SLAT_NCCL_KEEP(ctx, st, ncclGroupEnd());
+    if (st == SLAT_OK) st = assembly_finish(ctx, a, full, P);
+    cleanup();
+    if (st != SLAT_OK && full->row_ptr) {
+        (void)hipStreamSynchronize(s);
+        slat_csr_free(ctx, full);
+    }
+    return st;
+}
+
+extern "C" slat_status slat_concat_rows(slat_ctx *ctx, const slat_csr_view *blocks, uint32_t nblocks, slat_csr *full) {
+    if (!ctx || !full || (nblocks && !blocks)) return SLAT_EINVAL;
+    std::memset(full, 0, sizeof *full);
+    if (nblocks == 0) return fail(ctx, SLAT_EINVAL, "no blocks");
+    slat_status st;
+    for (uint32_t r = 0; r < nblocks; ++r) {
+        if ((st = slat_check_view(ctx, &blocks[r], "block"))) return st;
+        if (blocks[r].residency != SLAT_DEVICE) return fail(ctx, SLAT_EINVAL, "device views only");
+        if (blocks[r].n_cols != blocks[0].n_cols) return fail(ctx, SLAT_EDIM, "the row blocks differ in columns");
+    }
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    const hipStream_t s = ctx->stream;
+    const int P = (int)nblocks;
+    const int32_t dt = blocks[0].dtype;
+    std::vector<uint64_t> meta((size_t)4 * P), first(P, 0);
+    for (int r = 0; r < P; ++r) {
+        if (blocks[r].n_rows) SLAT_HIP(ctx, hipMemcpyAsync(&first[r], blocks[r].row_ptr, 8, hipMemcpyDeviceToHost, s));
+        meta[4 * r] = blocks[r].n_rows;
+        meta[4 * r + 1] = blocks[r].nnz;
+        meta[4 * r + 2] = blocks[r].max_row_nnz;
+        meta[4 * r + 3] = (uint64_t)blocks[r].dtype;
+    }
     SLAT_HIP(ctx, hipStreamSynchronize(s));
-    return SLAT_OK;
+    Assembly a;
+    if ((st = assembly_plan(ctx, meta.data(), P, dt, blocks[0].n_cols, a, full))) return st;
+    const size_t vs = vsize(dt);
+    std::vector<uint64_t *> tmps;
+    for (int r = 0; r < P && st == SLAT_OK; ++r) {
+        const slat_csr_view &b = blocks[r];
+        const uint64_t *ends = nullptr;
+        uint64_t *tmp = nullptr;
+        if ((st = rel_ends(ctx, &b, first[r], &ends, &tmp))) break;
+        if (tmp) tmps.push_back(tmp);
+        hipError_t e = hipSuccess;
+        if (b.n_rows)
+            e = hipMemcpyAsync(full->row_ptr + 1 + a.row_off[r], ends, b.n_rows * 8, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess && b.nnz)
+            e = hipMemcpyAsync(full->col_idx + a.nnz_off[r], (const uint8_t *)b.col_idx + first[r] * 4, b.nnz * 4,
+                               hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess && b.nnz)
+            e = hipMemcpyAsync((uint8_t *)full->values + a.nnz_off[r] * vs, (const uint8_t *)b.values + first[r] * vs,
+                               b.nnz * vs, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) st = fail(ctx, SLAT_EHIP, std::string("block copy: ") + hipGetErrorString(e));
+    }
+    if (st == SLAT_OK) st = assembly_finish(ctx, a, full, P);
+    if (a.tab) slat_dev_free(ctx, a.tab, s);
+    for (uint64_t *t : tmps) slat_dev_free(ctx, t, s);
+    if (st != SLAT_OK) {
+        (void)hipStreamSynchronize(s);
+        slat_csr_free(ctx, full);
+    }
+    return st;
 }

@@ -24,12 +24,14 @@
 // B is read in its CSR form; the B-row part inside a column range is found by a 64-ary search.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 
 #include "slat.h"
 #include "slat_internal.hpp"
 #include "spgemm_kernels.hpp"
+#include "slat_fat.hpp"
 
 namespace slat {
 
@@ -50,16 +52,6 @@ __host__ __device__ constexpr size_t fr_lds() {
 
 __device__ __forceinline__ uint32_t cap63(uint64_t x) { return x < 63 ? (uint32_t)x : 63u; }
 
-struct FatArgs {
-    Args a;
-    uint32_t *list;          // fat rows
-    unsigned int *cnt;       // their number
-    uint8_t *mark;           // [n] 1 = fat
-    unsigned long long *cmask;  // [list position] touched accumulator chunks (bit c: chunk c; 64 max)
-    uint32_t csh;            // log2 of the chunk mask's granule (columns per mask bit)
-};
-
-static_assert(sizeof(FatArgs) <= 1024, "slat_api.hip keeps FatArgs in a 1 KB buffer");
 
 // products of each row, cut off at kFat; fat rows marked and listed
 __global__ __launch_bounds__(kBlock) void k_fr_select(FatArgs f) {
@@ -406,11 +398,11 @@ slat_status slat_fat_symbolic(slat_ctx *ctx, FatArgs &f, const Args &a, bool idx
     f.a = a;
     const dim3 g((unsigned)ctx->cu_count);
     const size_t lds = kSymBits / 8 + kFW * 4 + kFW * 8;
-    static bool attr = false;
-    if (!attr) {  // more than 64 KB of dynamic LDS per block
+    static std::atomic<uint64_t> attr{0};  // devices whose attribute is set (idempotent, so a race is harmless)
+    if (!(attr.load(std::memory_order_relaxed) >> (ctx->device & 63) & 1)) {  // > 64 KB of dynamic LDS per block
         (void)hipFuncSetAttribute((const void *)k_fr_symbolic<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         (void)hipFuncSetAttribute((const void *)k_fr_symbolic<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
+        attr.fetch_or(1ull << (ctx->device & 63), std::memory_order_relaxed);
     }
     if (idx32)
         hipLaunchKernelGGL(k_fr_symbolic<uint32_t>, g, dim3(kFB), lds, ctx->stream, f);
@@ -427,11 +419,11 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
     // the chunk mask's granule must be a multiple of this instance's chunk
     FatArgs h = f;
     if ((1ull << h.csh) < fr_chunk<Sem>()) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {  // more than 64 KB of dynamic LDS per block
+    static std::atomic<uint64_t> attr{0};  // per device, as above
+    if (!(attr.load(std::memory_order_relaxed) >> (ctx->device & 63) & 1)) {  // > 64 KB of dynamic LDS per block
         (void)hipFuncSetAttribute((const void *)k_fr_numeric<Sem, uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         (void)hipFuncSetAttribute((const void *)k_fr_numeric<Sem, uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr = true;
+        attr.fetch_or(1ull << (ctx->device & 63), std::memory_order_relaxed);
     }
     if (idx32)
         hipLaunchKernelGGL((k_fr_numeric<Sem, uint32_t>), g, dim3(kFB), lds, ctx->stream, h);

@@ -1,0 +1,25 @@
+// slat_fat.hpp — the fat-row category's launch record and host entry points (slat_fat.hip), shared
+// with the SpGEMM orchestration (slat_api.hip).
+#pragma once
+#include <stdint.h>
+
+#include "slat_internal.hpp"
+#include "spgemm_kernels.hpp"
+
+namespace slat {
+struct FatArgs {
+    Args a;
+    uint32_t *list;             // fat rows
+    unsigned int *cnt;          // their number
+    uint8_t *mark;              // [n] 1 = fat
+    unsigned long long *cmask;  // [list position] touched accumulator chunks (bit c: chunk c; 64 max)
+    uint32_t csh;               // log2 of the chunk mask's granule (columns per mask bit)
+};
+}  // namespace slat
+
+// workspace bytes of the category for n rows
+size_t slat_fat_ws(uint64_t n);
+// mark and list the rows of >= 16384 products (sets a.fr_mark); nothing comes back to the host
+slat_status slat_fat_select(slat_ctx *ctx, slat::Args &a, void *ws, slat::FatArgs *out);
+slat_status slat_fat_symbolic(slat_ctx *ctx, slat::FatArgs &f, const slat::Args &a, bool idx32);
+slat_status slat_fat_numeric(slat_ctx *ctx, slat::FatArgs &f, const slat::Args &a, int32_t dtype, bool f64any, bool idx32);

@@ -114,18 +114,24 @@ extern "C" slat_status slat_magnus_matmul(slat_ctx *ctx, const slat_magnus_view 
     };
     slat_status st = narrow_view(ctx, A, "A", &va, &ta, &sa, bad);
     if (!st) st = narrow_view(ctx, B, "B", &vb, &tb, &sb, bad);
-    slat_csr c32 = {};
-    if (!st) st = slat_spgemm_csr_sat64(ctx, &va, &vb, &c32, flags);  // synchronous: *bad is final
     if (st) {
         release();
         return st;
     }
+    // the narrowing verdict before the product: an id >= n_cols (or >= 2^32, which would wrap to a
+    // valid-looking u32) must never reach the SpGEMM kernels' LDS bitmaps and composite keys
     unsigned int hbad = 0;
-    SLAT_HIP(ctx, hipMemcpy(&hbad, bad, 4, hipMemcpyDeviceToHost));
+    SLAT_HIP(ctx, hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
+    SLAT_HIP(ctx, hipStreamSynchronize(s));
     if (hbad) {
-        slat_csr_free(ctx, &c32);
         release();
         return fail(ctx, SLAT_EINVAL, "a column id is >= n_cols");
+    }
+    slat_csr c32 = {};
+    st = slat_spgemm_csr_sat64(ctx, &va, &vb, &c32, flags);  // synchronous
+    if (st) {
+        release();
+        return st;
     }
     uint64_t *c64 = nullptr;
     if (slat_dev_alloc(ctx, (void **)&c64, std::max<uint64_t>(c32.nnz, 1) * 8, s) != hipSuccess) {

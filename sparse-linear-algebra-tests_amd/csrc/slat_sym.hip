@@ -1,0 +1,31 @@
+// slat_sym.hip — the symbolic kernel instances (slat_launch.hpp), in a translation unit of their own
+// so they build beside the numeric ones.
+#include <hip/hip_runtime.h>
+
+#include "slat_launch.hpp"
+#include "spgemm_kernels.hpp"
+
+using namespace slat;
+
+hipError_t slat_launch_symbolic(int mode, bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, s, a);
+        return hipGetLastError();
+    };
+    if (mode == 1)
+        return idx32 ? (ell ? go(k_symbolic<uint32_t, true, 1>) : go(k_symbolic<uint32_t, false, 1>))
+                     : (ell ? go(k_symbolic<uint64_t, true, 1>) : go(k_symbolic<uint64_t, false, 1>));
+    if (mode == 2)
+        return idx32 ? (ell ? go(k_symbolic<uint32_t, true, 2>) : go(k_symbolic<uint32_t, false, 2>))
+                     : (ell ? go(k_symbolic<uint64_t, true, 2>) : go(k_symbolic<uint64_t, false, 2>));
+    return idx32 ? (ell ? go(k_symbolic<uint32_t, true>) : go(k_symbolic<uint32_t, false>))
+                 : (ell ? go(k_symbolic<uint64_t, true>) : go(k_symbolic<uint64_t, false>));
+}
+
+hipError_t slat_launch_symbolic_short(bool idx32, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
+    if (idx32)
+        hipLaunchKernelGGL(k_symbolic_short<uint32_t>, grid, dim3(kBlock), lds, s, a);
+    else
+        hipLaunchKernelGGL(k_symbolic_short<uint64_t>, grid, dim3(kBlock), lds, s, a);
+    return hipGetLastError();
+}

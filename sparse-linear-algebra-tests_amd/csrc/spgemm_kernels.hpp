@@ -94,12 +94,8 @@ struct Args {
     uint32_t *sbm;
     uint32_t *smask;
     uint32_t nblk;
-    // MAGNUS-style short-row category (wide launches): rows whose outputs fit a per-wave LDS hash
-    // table accumulate there and emit by rank-by-count instead of bitmap windows (0 = off)
-    uint32_t hash;
     uint32_t b_maxrow;
     uint32_t cbits;     // k_*_short: column bits of the composite (row, column) keys (0: one row per batch)
-    const uint32_t *rbound;  // experiment (short_sort.hpp): ELL groups per row, written by k_symbolic_sort
     // rows of the window category, appended by the short-row kernels (symbolic / numeric lists)
     // and walked by the MODE 2 launches instead of every row
     uint32_t *list;
@@ -1312,8 +1308,13 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
         atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
 }
 
+// variant builds: -DSLAT_NUM_WPE=w caps k_numeric's registers for w waves per SIMD
 #ifndef SLAT_NUM_ATTR
+#ifdef SLAT_NUM_WPE
+#define SLAT_NUM_ATTR __attribute__((amdgpu_waves_per_eu(SLAT_NUM_WPE)))
+#else
 #define SLAT_NUM_ATTR
+#endif
 #endif
 
 // MODE 0: every row by bitmap windows. Wide launches split the rows by output count (known from
@@ -1374,7 +1375,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
     auto mark = [&](int i) { pc.mark(i); };
     uint64_t *ph = pc.ph;
-    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short / _sort
+    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
@@ -1478,7 +1479,8 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                     //     nothing is cleared afterwards
                     bmask = __builtin_amdgcn_readfirstlane(p.smask[row]);
                     const uint32_t *src = p.sbm + row * ((uint64_t)p.nblk * kWave) + lane;
-                    for (uint32_t m = bmask; m;) {
+                    uint32_t m = bmask;
+                    while (m) {
                         uint32_t bs[8], xs[8];
                         sfor<8>([&](auto I_) {
                             bs[I_] = m ? (uint32_t)__builtin_ctz(m) : 32u;
@@ -1906,7 +1908,7 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
 
 // ------------------------------------------------------------------------------------------------
 // Wave-wide bitonic sort of 256 (key, payload) pairs, 4 per lane (element i = lane * 4 + e): the
-// emit order of the hash categories' keys (and the sorted short-row experiment, short_sort.hpp).
+// emit order of the hash categories' keys.
 // ------------------------------------------------------------------------------------------------
 // value of lane (lane ^ M): DPP quad permutes for 1 and 2 (bound_ctrl: no old value to set up, every
 // lane reads a valid source), ds_swizzle (bit-mask mode, within 32 lanes) up to 16, ds_bpermute for 32
@@ -2245,11 +2247,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     numeric_short_body<Sem0, I>(p);
 }
 // u32: 6 waves per SIMD (6.6 KB of LDS per wave, <= 80 VGPRs; the wider semirings are held to 4
-// waves by their LDS anyway)
+// waves by their LDS anyway). Variant builds: -DSLAT_SHORT_WPE=w (0: no cap).
+#ifndef SLAT_SHORT_WPE
+#define SLAT_SHORT_WPE 6
+#endif
 template <typename I>
 __global__ __launch_bounds__(kBlock)
-#ifndef SLAT_EXP_SHORT_W4
-__attribute__((amdgpu_waves_per_eu(6)))
+#if SLAT_SHORT_WPE
+__attribute__((amdgpu_waves_per_eu(SLAT_SHORT_WPE)))
 #endif
 void k_numeric_short_u32(Args p) {
     numeric_short_body<SemU32, I>(p);

@@ -29,7 +29,7 @@ EXPORTS = [
     "slat_bandwidth_stats", "slat_spgemm_dense", "slat_device_alloc", "slat_device_free", "slat_device_copy",
     "slat_magnus_matmul", "slat_magnus_free", "slat_magnus_to_host", "slat_magnus_view_of",
     "slat_comm_id", "slat_comm_create", "slat_comm_destroy", "slat_rowblock_cuts", "slat_bcast_csr",
-    "slat_allgather_rows", "slat_diameter", "slat_spgemm_btree",
+    "slat_allgather_rows", "slat_concat_rows", "slat_diameter", "slat_spgemm_btree",
 ]
 
 
@@ -167,6 +167,7 @@ def lib():
         "slat_rowblock_cuts": ([vp, P(CsrView), P(CsrView), u32, vp], C.c_int),
         "slat_bcast_csr": ([vp, vp, P(CsrOwned), C.c_int], C.c_int),
         "slat_allgather_rows": ([vp, vp, P(CsrView), P(CsrOwned)], C.c_int),
+        "slat_concat_rows": ([vp, P(CsrView), C.c_uint32, P(CsrOwned)], C.c_int),
         "slat_diameter": ([vp, P(CsrView), P(u64), P(u64), P(u64)], C.c_int),
         "slat_spgemm_btree": ([vp, P(BTreeView), P(BTreeView), P(CsrOwned), u32], C.c_int),
     }

@@ -104,6 +104,21 @@ def device_cuts(A, B, parts: int) -> list[int]:
     return [int(c) for c in cuts]
 
 
+def concat_rows(blocks, views=None):
+    """Row blocks living on one device stacked into one matrix (slat_concat_rows): the allgatherv's
+    assembly (offset tables, row ends taken relative to each block's first entry, rebase kernel)
+    without the transport. `views` may replace the blocks' own views (views into larger matrices)."""
+    import ctypes as C
+
+    from . import _lib as L
+    vs = views if views is not None else [b.view() for b in blocks]
+    arr = (L.CsrView * len(vs))(*vs)
+    out = L.CsrOwned()
+    ctx = blocks[0]._ctx
+    L.check(L.lib().slat_concat_rows(ctx.ptr, arr, len(vs), C.byref(out)), ctx.ptr)
+    return type(blocks[0])(out, ctx)
+
+
 def _to_i64(a: np.ndarray) -> np.ndarray:
     """Bit-preserving int64 view for transport (u32 widened, u64 / f64 reinterpreted)."""
     a = np.ascontiguousarray(a)

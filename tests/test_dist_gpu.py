@@ -1,7 +1,10 @@
 """The multi-GPU row-block path through libslat's C ABI on one GPU: device cuts
 equal the numpy restatement of the flops-balanced rule; a one-rank RCCL communicator's broadcast and
 allgatherv return the matrix they were given (row_ptr rebased, including a block given as a view
-with absolute offsets). Multi-rank RCCL needs one GPU per rank: the driver's 8-GPU run covers it."""
+with absolute offsets); the allgatherv's assembly (offset tables, relative row ends, the k_rebase
+kernel) over many blocks through slat_concat_rows. Multi-rank RCCL needs one GPU per rank: the
+driver's 8-GPU run covers it, and bench.py checks that run's gathered product against the golden
+digests."""
 import ctypes as C
 import os
 import socket
@@ -96,3 +99,38 @@ def test_one_rank_rccl_bcast_and_allgather(ctx, group, cls):
         _same(g2, blk)
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("cls", [slat.CsrMatrix, slat.MagnusMatrix, slat.CsrF64])
+@pytest.mark.parametrize("parts", [1, 2, 5, 8])
+def test_concat_row_blocks_equals_product(ctx, cls, parts):
+    """Flops-balanced row blocks of (A^2)·A computed apart, stacked by the rebase path: the full
+    product, bit for bit (several blocks, empty ones included when parts exceed the busy rows)."""
+    o = O.torus_thinned(20, 3.0, O.Rng())
+    rp, col, val = o.arrays()
+    A = cls.from_host(slat.HostCsr(o.n, rp, col, val, slat.U32).astype(cls.DTYPE), ctx)
+    P = A._spgemm(A)
+    full = P._spgemm(A)
+    cuts = D.device_cuts(P, A, parts)
+    blocks = [P.matmul_rowblock(cuts[r], cuts[r + 1], A) for r in range(parts)]
+    got = D.concat_rows(blocks)
+    _same(got, full)
+    assert got.nnz() == full.nnz() and got.max_row_nnz == full.max_row_nnz
+    # blocks given as views with absolute offsets into the full product, plus an empty block
+    h = full.host()
+    edges = [0, 1, 1, 2000, 4000, 4001, 8000, o.n]
+    views = []
+    for a, b in zip(edges[:-1], edges[1:]):
+        v = full.view()
+        v.row_ptr = v.row_ptr + 8 * a
+        v.n_rows = b - a
+        v.nnz = int(h.row_ptr[b] - h.row_ptr[a])
+        views.append(v)
+    _same(D.concat_rows([full] * len(views), views), full)
+
+
+def test_concat_rows_refuses_mixed_blocks(ctx):
+    a = slat.CsrMatrix.from_host(slat.torus_thinned(5, 3.0, slat.StdRng()), ctx)
+    b = slat.CsrF64.from_host(slat.torus_thinned(5, 3.0, slat.StdRng()).astype(slat.F64), ctx)
+    with pytest.raises(slat.SlatError):
+        D.concat_rows([a, b])

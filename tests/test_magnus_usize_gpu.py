@@ -52,14 +52,33 @@ def test_saturating_values_usize_cols():
     _check(slat.MagnusMatrixUsize.matmul_host(va, va), O.matmul_seq(A, A))
 
 
-def test_column_out_of_range_is_an_error():
+@pytest.mark.parametrize("bad_id", [2**32 + 1, 2, 70_000, 2**32 - 1])
+def test_column_out_of_range_is_an_error(bad_id):
+    """An id no u32 can hold (2^32 + 1 would wrap to the valid id 1) and ids in [n_cols, 2^32) are
+    refused before the product runs, with the context still usable afterwards."""
     rp = np.array([0, 1, 1], np.uint64)
-    col = np.array([2**32 + 1], np.uint64)  # a usize id no u32 can hold
+    col = np.array([bad_id], np.uint64)
     val = np.array([1], np.uint64)
     v = slat.MagnusMatrixUsize.host_view(2, rp, col, val)
     with pytest.raises(slat.SlatError) as e:
         slat.MagnusMatrixUsize.matmul_host(v, v)
     assert e.value.status == 1  # SLAT_EINVAL (the reference would index out of bounds and panic)
+    # a wide B (80 000 columns: the LDS-hash and window categories) with one id past n_cols in A
+    n = 80_000
+    brp = np.arange(n + 1, dtype=np.uint64)
+    bcol = np.arange(n, dtype=np.uint64)[::-1].copy()
+    one = np.ones(n, np.uint64)
+    vb = slat.MagnusMatrixUsize.host_view(n, brp, bcol, one)
+    acol = np.array([5, n + 7], np.uint64)
+    va = slat.MagnusMatrixUsize.host_view(n, np.array([0] + [2] * n, np.uint64), acol, np.ones(2, np.uint64))
+    with pytest.raises(slat.SlatError) as e:
+        slat.MagnusMatrixUsize.matmul_host(va, vb)
+    assert e.value.status == 1
+    # and a valid product right after the refusals
+    A = O.convert(O.torus_thinned(10, 3.0, O.Rng()), O.SAT64)
+    a = _arrays(A)
+    va = slat.MagnusMatrixUsize.host_view(A.n, *a)
+    _check(slat.MagnusMatrixUsize.matmul_host(va, va), O.matmul_seq(A, A))
 
 
 def test_dimension_mismatch_usize():

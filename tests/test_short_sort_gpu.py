@@ -1,7 +1,5 @@
-"""The short-row categories of wide launches: the batched LDS hash tables (default) and the opt-in
-register sort (SLAT_SORT_SHORT=1, csrc/short_sort.hpp: a batch of
-consecutive rows with <= 64 ELL groups and <= 256 A entries, one group per lane, a bitonic sort
-over the wave, run sums by a segmented scan). Bit-exact against the oracle for u32 / Sat64, and
+"""The short-row category of wide launches: batches of consecutive short rows in one LDS hash table
+of composite (row, column) keys, emitted by a wave bitonic sort. Bit-exact against the oracle for u32 / Sat64, and
 within C5's stated tolerance (rtol 1e-12) for f64 in any order. Cases at the category's edges:
 64 / 65 groups and 256 / 257 entries per row, runs of 64 equal keys (every group of the batch
 hits the same columns), A entries into empty B rows, explicit zeros and saturation, and one row
@@ -184,18 +182,3 @@ def test_row_bounds_with_long_rows_at_chunk_edges():
              for r in range(6300, 6700) if r not in taken]
     A = from_rows(N, rows, O.U32, rng)
     assert_same(to_dev(A, slat.CsrMatrix)._spgemm(to_dev(B, slat.CsrMatrix)), O.matmul_seq(A, B), "chunk edges")
-
-
-def test_register_sort_experiment_path():
-    """The opt-in register-sorted category (SLAT_SORT_SHORT=1 is read once per process): the edge cases
-    above in a child process with it on."""
-    import os
-    import subprocess
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, SLAT_SORT_SHORT="1")
-    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
-                        os.path.join(here, "test_short_sort_gpu.py"), "-k",
-                        "category_edges or zeros_and_saturation or sat64_saturating or chunk_edges or one_row_per_batch"],
-                       env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

@@ -1,11 +1,8 @@
 #!/bin/bash
-# usage: tools/build_variant.sh NAME SRC "-DFLAG=..." — builds tools/bin/libslat_NAME.so with SRC
-# (e.g. slat_fused) compiled with the extra flags and the tree's other objects (kernel experiments)
+# usage: tools/build_variant.sh NAME "-DFLAG=... ..." — builds tools/var/libslat_NAME.so: the whole
+# library with the extra compiler flags, in its own object directory (kernel experiments; load it
+# with SLAT_LIB_PATH=tools/var/libslat_NAME.so)
 set -e
-mkdir -p "$(dirname "$0")/bin"
-cd "$(dirname "$0")/../sparse-linear-algebra-tests_amd"
-make -s
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -I../include -Icsrc $3 -c csrc/$2.hip -o /tmp/slat_$1.o
-objs=""
-for o in $(sed -n "s/^libslat.so: //p" Makefile); do [ "$o" = "build/$2.o" ] || objs="$objs $o"; done
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../tools/bin/libslat_$1.so /tmp/slat_$1.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+root="$(cd "$(dirname "$0")/.." && pwd)"
+mkdir -p "$root/tools/var"
+make -s -j8 -C "$root/sparse-linear-algebra-tests_amd" BUILD=/tmp/slat_var_$1 "EXTRA=$2" OUT="$root/tools/var/libslat_$1.so"
