@@ -75,7 +75,7 @@ def main():
             env = dict(os.environ)
             env.pop("SLAT_LIB_PATH", None)
             if name != "tree":
-                env["SLAT_LIB_PATH"] = os.path.join(ROOT, "tools", "bin", f"libslat_{name}.so")
+                env["SLAT_LIB_PATH"] = os.path.join(ROOT, "tools", "var", f"libslat_{name}.so")
             for kv in filter(None, knobs.split(",")):
                 k, _, val = kv.partition("=")
                 env[k] = val
