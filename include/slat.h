@@ -185,6 +185,15 @@ typedef struct {
 slat_status slat_magnus_matmul(slat_ctx *ctx, const slat_magnus_view *A, const slat_magnus_view *B,
                                slat_magnus *C, uint32_t flags);
 slat_status slat_magnus_free(slat_ctx *ctx, slat_magnus *m);
+/* MagnusMatrix's SpGEMM consumers in the same layout (src/graph_magnus.rs:245-359): add (per-row
+ * sorted union, Sat64 sums, exact zeros dropped), reachability_sum (A + A^2 + ... until nnz repeats;
+ * *k = last power), power_until_stable (repeated squaring until the pattern is stable; *k =
+ * squarings) and connected_components (closure of A + I; `component` = host array of n_rows u64).
+ * The same device kernels as the u32-column entry points, with the columns narrowed / widened. */
+slat_status slat_magnus_add(slat_ctx *ctx, const slat_magnus_view *A, const slat_magnus_view *B, slat_magnus *C);
+slat_status slat_magnus_reachability_sum(slat_ctx *ctx, const slat_magnus_view *A, slat_magnus *sum, uint64_t *k);
+slat_status slat_magnus_power_until_stable(slat_ctx *ctx, const slat_magnus_view *A, slat_magnus *out, uint64_t *k);
+slat_status slat_magnus_connected_components(slat_ctx *ctx, const slat_magnus_view *A, uint64_t *component);
 slat_status slat_magnus_to_host(slat_ctx *ctx, const slat_magnus *m, uint64_t *row_ptr, uint64_t *col_idx,
                                 uint64_t *values);
 slat_magnus_view slat_magnus_view_of(const slat_magnus *m);

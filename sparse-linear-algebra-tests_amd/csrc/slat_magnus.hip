@@ -91,14 +91,11 @@ slat_status narrow_view(slat_ctx *ctx, const slat_magnus_view *m, const char *na
     return SLAT_OK;
 }
 
-}  // namespace
-
-extern "C" slat_status slat_magnus_matmul(slat_ctx *ctx, const slat_magnus_view *A, const slat_magnus_view *B,
-                                          slat_magnus *C, uint32_t flags) {
-    if (!ctx || !C) return SLAT_EINVAL;
-    SLAT_HIP(ctx, hipSetDevice(ctx->device));
-    std::memset(C, 0, sizeof *C);
-    if (A && B && A->n_cols != B->n_rows) return fail(ctx, SLAT_EDIM, "A.n_cols != B.n_rows");
+// The MagnusMatrix operations in its own layout: the inputs' u64 column ids are narrowed on the
+// device (an id >= n_cols refused before anything runs), `op` runs on the u32-column Sat64 views,
+// and its result's columns are widened back into *C (row_ptr and values stay in op's block).
+template <typename Op>
+slat_status magnus_op(slat_ctx *ctx, const slat_magnus_view *A, const slat_magnus_view *B, slat_magnus *C, Op &&op) {
     const hipStream_t s = ctx->stream;
     // the narrowing kernels' error word: a context scratch word, cleared on the stream
     unsigned int *bad = (unsigned int *)(ctx->d_words + 4);
@@ -113,13 +110,13 @@ extern "C" slat_status slat_magnus_matmul(slat_ctx *ctx, const slat_magnus_view 
         if (sb.row_ptr) slat_csr_free(ctx, &sb);
     };
     slat_status st = narrow_view(ctx, A, "A", &va, &ta, &sa, bad);
-    if (!st) st = narrow_view(ctx, B, "B", &vb, &tb, &sb, bad);
+    if (!st && B) st = narrow_view(ctx, B, "B", &vb, &tb, &sb, bad);
     if (st) {
         release();
         return st;
     }
-    // the narrowing verdict before the product: an id >= n_cols (or >= 2^32, which would wrap to a
-    // valid-looking u32) must never reach the SpGEMM kernels' LDS bitmaps and composite keys
+    // the narrowing verdict before the operation: an id >= n_cols (or >= 2^32, which would wrap to
+    // a valid-looking u32) must never reach the kernels' LDS bitmaps and composite keys
     unsigned int hbad = 0;
     SLAT_HIP(ctx, hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
     SLAT_HIP(ctx, hipStreamSynchronize(s));
@@ -128,10 +125,15 @@ extern "C" slat_status slat_magnus_matmul(slat_ctx *ctx, const slat_magnus_view 
         return fail(ctx, SLAT_EINVAL, "a column id is >= n_cols");
     }
     slat_csr c32 = {};
-    st = slat_spgemm_csr_sat64(ctx, &va, &vb, &c32, flags);  // synchronous
+    st = op(&va, B ? &vb : nullptr, &c32);  // synchronous
     if (st) {
         release();
         return st;
+    }
+    if (!C) {  // no matrix result (connected components)
+        release();
+        if (c32.row_ptr) slat_csr_free(ctx, &c32);
+        return SLAT_OK;
     }
     uint64_t *c64 = nullptr;
     if (slat_dev_alloc(ctx, (void **)&c64, std::max<uint64_t>(c32.nnz, 1) * 8, s) != hipSuccess) {
@@ -155,6 +157,61 @@ extern "C" slat_status slat_magnus_matmul(slat_ctx *ctx, const slat_magnus_view 
     static_assert(sizeof(slat_csr) <= sizeof(C->_owner), "slat_magnus owner slot too small");
     std::memcpy(C->_owner, &c32, sizeof c32);
     return SLAT_OK;
+}
+
+}  // namespace
+
+extern "C" slat_status slat_magnus_matmul(slat_ctx *ctx, const slat_magnus_view *A, const slat_magnus_view *B,
+                                          slat_magnus *C, uint32_t flags) {
+    if (!ctx || !C) return SLAT_EINVAL;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    std::memset(C, 0, sizeof *C);
+    if (!B) return fail(ctx, SLAT_EINVAL, "B is null");
+    if (A && A->n_cols != B->n_rows) return fail(ctx, SLAT_EDIM, "A.n_cols != B.n_rows");
+    return magnus_op(ctx, A, B, C, [&](const slat_csr_view *a, const slat_csr_view *b, slat_csr *c) {
+        return slat_spgemm_csr_sat64(ctx, a, b, c, flags);
+    });
+}
+
+extern "C" slat_status slat_magnus_add(slat_ctx *ctx, const slat_magnus_view *A, const slat_magnus_view *B,
+                                       slat_magnus *C) {
+    if (!ctx || !C) return SLAT_EINVAL;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    std::memset(C, 0, sizeof *C);
+    if (!B) return fail(ctx, SLAT_EINVAL, "B is null");
+    // assert_eq!(self.n, other.n) (src/graph_magnus.rs:246)
+    if (A && (A->n_rows != B->n_rows || A->n_cols != B->n_cols)) return fail(ctx, SLAT_EDIM, "A and B differ in shape");
+    return magnus_op(ctx, A, B, C, [&](const slat_csr_view *a, const slat_csr_view *b, slat_csr *c) {
+        return slat_csr_add(ctx, a, b, c);
+    });
+}
+
+extern "C" slat_status slat_magnus_reachability_sum(slat_ctx *ctx, const slat_magnus_view *A, slat_magnus *sum,
+                                                    uint64_t *k) {
+    if (!ctx || !sum || !k) return SLAT_EINVAL;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    std::memset(sum, 0, sizeof *sum);
+    return magnus_op(ctx, A, nullptr, sum, [&](const slat_csr_view *a, const slat_csr_view *, slat_csr *c) {
+        return slat_reachability_sum(ctx, a, c, k);
+    });
+}
+
+extern "C" slat_status slat_magnus_power_until_stable(slat_ctx *ctx, const slat_magnus_view *A, slat_magnus *out,
+                                                      uint64_t *k) {
+    if (!ctx || !out || !k) return SLAT_EINVAL;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    std::memset(out, 0, sizeof *out);
+    return magnus_op(ctx, A, nullptr, out, [&](const slat_csr_view *a, const slat_csr_view *, slat_csr *c) {
+        return slat_power_until_stable(ctx, a, c, k);
+    });
+}
+
+extern "C" slat_status slat_magnus_connected_components(slat_ctx *ctx, const slat_magnus_view *A, uint64_t *component) {
+    if (!ctx || !component) return SLAT_EINVAL;
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    return magnus_op(ctx, A, nullptr, nullptr, [&](const slat_csr_view *a, const slat_csr_view *, slat_csr *) {
+        return slat_connected_components(ctx, a, component);
+    });
 }
 
 extern "C" slat_status slat_magnus_free(slat_ctx *ctx, slat_magnus *m) {

@@ -28,6 +28,8 @@ EXPORTS = [
     "slat_load_edges", "slat_edges_free", "slat_csr_from_edges", "slat_rcm_order", "slat_csr_permute",
     "slat_bandwidth_stats", "slat_spgemm_dense", "slat_device_alloc", "slat_device_free", "slat_device_copy",
     "slat_magnus_matmul", "slat_magnus_free", "slat_magnus_to_host", "slat_magnus_view_of",
+    "slat_magnus_add", "slat_magnus_reachability_sum", "slat_magnus_power_until_stable",
+    "slat_magnus_connected_components",
     "slat_comm_id", "slat_comm_create", "slat_comm_destroy", "slat_rowblock_cuts", "slat_bcast_csr",
     "slat_allgather_rows", "slat_concat_rows", "slat_diameter", "slat_spgemm_btree",
 ]
@@ -161,6 +163,10 @@ def lib():
         "slat_magnus_free": ([vp, P(MagnusOwned)], C.c_int),
         "slat_magnus_to_host": ([vp, P(MagnusOwned), vp, vp, vp], C.c_int),
         "slat_magnus_view_of": ([P(MagnusOwned)], MagnusView),
+        "slat_magnus_add": ([vp, P(MagnusView), P(MagnusView), P(MagnusOwned)], C.c_int),
+        "slat_magnus_reachability_sum": ([vp, P(MagnusView), P(MagnusOwned), P(C.c_uint64)], C.c_int),
+        "slat_magnus_power_until_stable": ([vp, P(MagnusView), P(MagnusOwned), P(C.c_uint64)], C.c_int),
+        "slat_magnus_connected_components": ([vp, P(MagnusView), vp], C.c_int),
         "slat_comm_id": ([vp], C.c_int),
         "slat_comm_create": ([vp, C.c_int, C.c_int, vp, P(vp)], C.c_int),
         "slat_comm_destroy": ([vp], C.c_int),

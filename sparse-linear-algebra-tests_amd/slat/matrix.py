@@ -589,6 +589,38 @@ class MagnusMatrixUsize:
 
     matmul_seq = matmul  # src/graph_magnus.rs:235-242: the same product
 
+    def add(self, other: "MagnusMatrixUsize") -> "MagnusMatrixUsize":
+        """MagnusMatrix::add (src/graph_magnus.rs:245-300): per-row sorted union, Sat64 sums."""
+        return MagnusMatrixUsize.add_host(self.view(), other.view(), self._ctx)
+
+    @staticmethod
+    def add_host(a: L.MagnusView, b: L.MagnusView, ctx: Context | None = None) -> "MagnusMatrixUsize":
+        ctx = ctx or default_context()
+        out = L.MagnusOwned()
+        L.check(L.lib().slat_magnus_add(ctx.ptr, C.byref(a), C.byref(b), C.byref(out)), ctx.ptr)
+        return MagnusMatrixUsize(out, ctx)
+
+    def reachability_sum(self):
+        """MagnusMatrix::reachability_sum (src/graph_magnus.rs:303-317): (sum, k)."""
+        out, k = L.MagnusOwned(), C.c_uint64()
+        v = self.view()
+        L.check(L.lib().slat_magnus_reachability_sum(self._ctx.ptr, C.byref(v), C.byref(out), C.byref(k)), self._ctx.ptr)
+        return MagnusMatrixUsize(out, self._ctx), int(k.value)
+
+    def power_until_stable(self):
+        """MagnusMatrix::power_until_stable (src/graph_magnus.rs:320-335): (closure, squarings)."""
+        out, k = L.MagnusOwned(), C.c_uint64()
+        v = self.view()
+        L.check(L.lib().slat_magnus_power_until_stable(self._ctx.ptr, C.byref(v), C.byref(out), C.byref(k)), self._ctx.ptr)
+        return MagnusMatrixUsize(out, self._ctx), int(k.value)
+
+    def connected_components(self) -> list:
+        """MagnusMatrix::connected_components (src/graph_magnus.rs:338-359): usize component ids."""
+        comp = np.zeros(self.n, np.uint64)
+        v = self.view()
+        L.check(L.lib().slat_magnus_connected_components(self._ctx.ptr, C.byref(v), comp.ctypes.data), self._ctx.ptr)
+        return [int(c) for c in comp]
+
     @property
     def n(self) -> int:
         return int(self._m.n_rows)
@@ -638,39 +670,116 @@ class CsrF64(Csr):
     DTYPE = L.F64
 
 
+KEYS_PER_NODE = 16  # src/dense_btree.rs:2
+MAX_BTREE_HEIGHT = 8  # src/dense_btree.rs:3
+
+
+def btree_levels(n: int):
+    """compute_levels (src/dense_btree.rs:9-42): (height, level sizes, level starts) of the compact
+    K-ary separator tree over n sorted keys; level 0 is the root."""
+    kpn = KEYS_PER_NODE
+    leaf_count = (n + kpn - 1) // kpn
+    sizes, starts = [0] * MAX_BTREE_HEIGHT, [0] * MAX_BTREE_HEIGHT
+    if leaf_count <= 1:
+        return 0, sizes, starts
+    stack, count = [], leaf_count
+    while count > 1:
+        count = (count + kpn - 1) // kpn
+        stack.append(count)
+    height = len(stack)
+    for i in range(height):
+        sizes[i] = stack[height - 1 - i]
+    start = 0
+    for i in range(height):
+        starts[i] = start
+        start += sizes[i] * kpn
+    return height, sizes, starts
+
+
+def btree_internal(values: np.ndarray) -> np.ndarray:
+    """The separator nodes DenseBTree::extend_from_sorted (src/dense_btree.rs:116-162) writes before
+    a row's sorted data: the bottom internal level holds each leaf chunk's last key, every upper
+    level each child node's last key, padding with the row's max key. Empty for <= 16 keys."""
+    n, kpn = len(values), KEYS_PER_NODE
+    if (n + kpn - 1) // kpn <= 1:
+        return np.zeros(0, values.dtype)
+    height, sizes, starts = btree_levels(n)
+    internal_len = starts[height - 1] + sizes[height - 1] * kpn
+    nodes = np.full(internal_len, values[n - 1], values.dtype)
+    bottom = height - 1
+    chunk = np.arange(sizes[bottom] * kpn)
+    nodes[starts[bottom]:starts[bottom] + len(chunk)] = values[np.minimum((chunk + 1) * kpn, n) - 1]
+    for level in range(bottom - 1, -1, -1):
+        child = np.arange(sizes[level] * kpn)
+        ok = child < sizes[level + 1]
+        base = starts[level]
+        nodes[base:base + len(child)][ok] = nodes[starts[level + 1] + child[ok] * kpn + kpn - 1]
+    return nodes
+
+
+def btree_index(nodes: np.ndarray, internal_len: int, value: int):
+    """DenseBTree::index (src/dense_btree.rs:176-205) over one row's [separators | data]: ("ok", i)
+    on an exact match, ("err", i) with the insertion point otherwise (slice::binary_search's
+    answer)."""
+    n = len(nodes) - internal_len
+    if n == 0:
+        return ("err", 0)
+    if value > nodes[-1]:
+        return ("err", n)
+    height, _, starts = btree_levels(n)
+    node = 0
+    for level in range(height):
+        base = starts[level] + node * KEYS_PER_NODE
+        node = node * KEYS_PER_NODE + int(np.count_nonzero(value > nodes[base:base + KEYS_PER_NODE]))
+    c0 = internal_len + node * KEYS_PER_NODE
+    c1 = min(c0 + KEYS_PER_NODE, len(nodes))
+    for i in range(c0, c1):
+        if nodes[i] == value:
+            return ("ok", i - internal_len)
+        if nodes[i] > value:
+            return ("err", i - internal_len)
+    return ("err", c1 - internal_len)
+
+
 class CsrBTreeMatrix:
     """`CsrBTreeMatrix` (src/graph_csr_btree.rs:44-52) in its host layout: DenseBTreeList's flat
-    `nodes` (every row as [separator nodes | sorted data], src/dense_btree.rs:269-330), the flat
-    `values`, and per row data_start (NodeEntry::data_start, plus total_data_len() at the end) and
-    data_off (offset + internal_len). matmul_par runs on the MI355X engine through
-    slat_spgemm_btree, which reads only the data slices.
+    `nodes` (every row as [separator nodes | sorted data], src/dense_btree.rs:269-330, the
+    separators built exactly as DenseBTree::extend_from_sorted does), the flat `values`, and per
+    row data_start (NodeEntry::data_start, plus total_data_len() at the end), data_off (offset +
+    internal_len) and internal_len. matmul_par runs on the MI355X engine through
+    slat_spgemm_btree, which reads only the data slices."""
 
-    The separators built here are a one-level index (every 16th key of the row after the first),
-    a stand-in for DenseBTree::extend_from_sorted's levels: the engine never reads them, and the
-    tests only need them to sit between the rows' data as in the reference's layout."""
-
-    def __init__(self, n: int, nodes, values, data_start, data_off, ctx: Context | None = None):
+    def __init__(self, n: int, nodes, values, data_start, data_off, ctx: Context | None = None, internal_len=None):
         self.n = int(n)
         self.nodes = np.ascontiguousarray(nodes, np.uint32)
         self.values = np.ascontiguousarray(values, np.uint32)
         self.data_start = np.ascontiguousarray(data_start, np.uint64)
         self.data_off = np.ascontiguousarray(data_off, np.uint64)
+        self.internal_len = None if internal_len is None else np.ascontiguousarray(internal_len, np.uint64)
         self._ctx = ctx or default_context()
 
     @classmethod
     def from_flat(cls, n: int, row_ptr, col_idx, values, ctx: Context | None = None) -> "CsrBTreeMatrix":
-        """CsrBTreeMatrix::from_flat (src/graph_csr_btree.rs:57-63): one tree per row, in row order."""
+        """CsrBTreeMatrix::from_flat (src/graph_csr_btree.rs:57-63): DenseBTreeList::add_from_sorted
+        of every row in row order (src/dense_btree.rs:286-293)."""
         row_ptr = np.asarray(row_ptr, np.uint64)
         col_idx = np.asarray(col_idx, np.uint32)
-        parts, offs, pos = [], np.zeros(n, np.uint64), 0
+        parts, offs, ilen, pos = [], np.zeros(n, np.uint64), np.zeros(n, np.uint64), 0
         for r in range(n):
             data = col_idx[int(row_ptr[r]):int(row_ptr[r + 1])]
-            sep = data[16::16]
+            sep = btree_internal(data)
             parts += [sep, data]
             offs[r] = pos + len(sep)
+            ilen[r] = len(sep)
             pos += len(sep) + len(data)
         nodes = np.concatenate(parts) if parts else np.zeros(0, np.uint32)
-        return cls(n, nodes, values, row_ptr, offs, ctx)
+        return cls(n, nodes, values, row_ptr, offs, ctx, ilen)
+
+    def index(self, r: int, value: int):
+        """DenseBTreeList::index (src/dense_btree.rs:306-309): DenseBTree::index within row r."""
+        il = int(self.internal_len[r])
+        o = int(self.data_off[r]) - il
+        return btree_index(self.nodes[o:int(self.data_off[r]) + int(self.data_start[r + 1] - self.data_start[r])], il, value)
 
     @classmethod
     def from_host(cls, h: HostCsr, ctx: Context | None = None) -> "CsrBTreeMatrix":

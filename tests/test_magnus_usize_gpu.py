@@ -89,3 +89,49 @@ def test_dimension_mismatch_usize():
     with pytest.raises(slat.SlatError) as ex:
         slat.MagnusMatrixUsize.matmul_host(a, b)
     assert ex.value.status == 2
+
+
+def _usize(o: O.Csr):
+    rp, col, val = _arrays(o)
+    return slat.MagnusMatrixUsize.host_view(o.n, rp, col, val), (rp, col, val)
+
+
+def test_add_and_drivers_usize_cols():
+    """MagnusMatrix::add / reachability_sum / power_until_stable / connected_components
+    (src/graph_magnus.rs:245-359) in the usize layout, bit-exact against the oracle's Sat64 restatement
+    of the CsrMatrix drivers (the reference's MagnusMatrix versions are the same algorithms)."""
+    A = O.convert(O.torus_thinned(8, 3.0, O.Rng()), O.SAT64)
+    va, keep = _usize(A)
+    M = slat.MagnusMatrixUsize.matmul_host(va, va)  # A^2, device-resident
+    got = M.add(M)
+    _check(got, O.add(O.matmul_seq(A, A), O.matmul_seq(A, A)))
+    ga = slat.MagnusMatrixUsize.add_host(va, va)
+    _check(ga, O.add(A, A))
+    s, k = ga.reachability_sum()
+    ws, wk = O.reachability_sum(O.add(A, A))
+    assert k == wk
+    _check(s, ws)
+    c, k = ga.power_until_stable()
+    wc, wk = O.power_until_stable(O.add(A, A))
+    assert k == wk
+    _check(c, wc)
+    assert ga.connected_components() == [int(x) for x in O.connected_components(O.add(A, A))]
+
+
+def test_saturating_chain_usize():
+    """The reference's 64-node chain (I + N) squared until stable (src/graph_csr.rs:931-939 and its
+    MagnusMatrix twin): 7 squarings, 1176 entries saturated at u64::MAX in Sat64 (SURVEY.md
+    section 8(c), golden 2), bit-exact against the oracle."""
+    n = 64
+    rows = np.concatenate([np.arange(n), np.arange(n - 1)])
+    cols = np.concatenate([np.arange(n), np.arange(1, n)])
+    A = O.from_coo(n, rows, cols, np.ones(len(rows), np.uint64), O.SAT64)
+    va, keep = _usize(A)
+    eye = np.arange(n + 1, dtype=np.uint64), np.arange(n, dtype=np.uint64), np.ones(n, np.uint64)
+    dev = slat.MagnusMatrixUsize.matmul_host(va, slat.MagnusMatrixUsize.host_view(n, *eye))  # A on the device
+    c, k = dev.power_until_stable()
+    wc, wk = O.power_until_stable(A)
+    assert k == wk == 7
+    _check(c, wc)
+    _, _, val = c.host()
+    assert int((val == np.uint64(2**64 - 1)).sum()) == 1176

@@ -19,14 +19,14 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(c4: bool, steps: int):
+def child(c4: bool, steps: int, only_c4: bool = False):
     sys.path.insert(0, os.path.join(ROOT, "sparse-linear-algebra-tests_amd"))
     import numpy as np
 
     import slat
     ctx = slat.Context(0)
     out = {}
-    legs = [("a7", 30, 7, steps)] + ([("c4", 100, 4, max(10, steps // 10))] if c4 else [])
+    legs = ([] if only_c4 else [("a7", 30, 7, steps)]) + ([("c4", 100, 4, max(10, steps // 10))] if c4 or only_c4 else [])
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
     for name, side, power, k in legs:
         A = slat.torus_thinned_device(side, 3.0, slat.StdRng(), ctx)
@@ -62,10 +62,11 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--c4", action="store_true")
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--only-c4", action="store_true", help="child: the C4 leg alone")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     if a.child:
-        child(a.c4, a.steps)
+        child(a.c4, a.steps, a.only_c4)
         return
     res = {}
     for r in range(a.reps):
