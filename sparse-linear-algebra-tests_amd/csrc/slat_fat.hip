@@ -109,7 +109,8 @@ __device__ __forceinline__ void b_range(const uint32_t *bcol, I bs, I be, uint32
 // once (2 kQ independent loads in flight), a longer one by the whole wave over its part in [lo, hi).
 constexpr int kQ = 4;
 template <typename S, bool VALS, typename I, typename F>
-__device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, uint32_t hi, bool all_cols, F &&fn) {
+__device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, uint32_t hi, bool all_cols, F &&fn,
+                                        const uint32_t *split = nullptr, uint32_t nch1 = 0, uint32_t chunk = 0) {
     const int lane = lane_id();
     const int wv = threadIdx.x / kWave;
     const S *av = (const S *)p.a_val;
@@ -130,10 +131,18 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
         sfor<kQ>([&](auto Q) {
             bs[Q] = be[Q] = 0;
             if (k[Q] < p.b_nrows) {
-                bs[Q] = (I)p.b_rp[k[Q]];
-                be[Q] = (I)p.b_rp[k[Q] + 1];
+                if (split) {  // only the chunk's part of the B row: no filtering, no search
+                    const I r = (I)p.b_rp[k[Q]];
+                    const uint32_t *sp = split + (uint64_t)k[Q] * nch1 + chunk;
+                    bs[Q] = r + (I)sp[0];
+                    be[Q] = r + (I)sp[1];
+                } else {
+                    bs[Q] = (I)p.b_rp[k[Q]];
+                    be[Q] = (I)p.b_rp[k[Q] + 1];
+                }
             }
         });
+        if (split) all_cols = true;
         uint32_t len[kQ], mx = 0;
         sfor<kQ>([&](auto Q) {
             const uint64_t l = (uint64_t)(be[Q] - bs[Q]);
@@ -172,6 +181,32 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
                 }
             });
         }
+    }
+}
+
+// the split table of B by accumulator chunk (FatArgs::split): thread per (row k, boundary c), a
+// binary search in the sorted row; boundary 0 is 0 and boundary nch1 - 1 the row length
+__global__ __launch_bounds__(kBlock) void k_fr_splits(const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb,
+                                                       uint32_t nch1, uint32_t chunk_shift, uint32_t *split) {
+    const uint64_t total = nb * nch1;
+    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = g / nch1;
+        const uint32_t c = (uint32_t)(g - k * nch1);
+        const uint64_t s = b_rp[k], e = b_rp[k + 1];
+        uint64_t lo = s, hi = e;
+        if (c == 0) {
+            hi = s;
+        } else if (c + 1 < nch1) {
+            const uint64_t key = (uint64_t)c << chunk_shift;  // first index with col >= key
+            while (lo < hi) {
+                const uint64_t mid = lo + (hi - lo) / 2;
+                if ((uint64_t)b_col[mid] < key)
+                    lo = mid + 1;
+                else
+                    hi = mid;
+            }
+        }
+        split[g] = (uint32_t)(hi - s);
     }
 }
 
@@ -248,9 +283,10 @@ __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
 // lanes over A entries. f64 in the reference's order: wave w owns columns [c0 + w*span, ...) and
 // walks the A entries in order, lanes over one B row (distinct columns): one writer per column.
 template <typename Sem, typename I>
-__device__ __forceinline__ void fr_accumulate(const Args &p, I a0, I a1, uint32_t c0, uint32_t c1,
+__device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint32_t c0, uint32_t c1,
                                               typename Sem::V *acc, uint32_t *bits) {
     using S = typename Sem::S;
+    const Args &p = f.a;
     const S *av = (const S *)p.a_val;
     const S *bv = (const S *)p.b_val;
     if constexpr (!Sem::kOrdered) {
@@ -259,7 +295,7 @@ __device__ __forceinline__ void fr_accumulate(const Args &p, I a0, I a1, uint32_
             const uint32_t o = c - c0;
             Sem::acc(acc, o, Sem::prod(a, b));
             atomicOr(&bits[o >> 5], 1u << (o & 31));
-        });
+        }, f.split, f.nch1, c0 / fr_chunk<Sem>());
     } else {
         const int lane = lane_id(), wv = threadIdx.x / kWave;
         const uint32_t span = (c1 - c0 + kFW - 1) / kFW;
@@ -274,8 +310,15 @@ __device__ __forceinline__ void fr_accumulate(const Args &p, I a0, I a1, uint32_
                 k = p.a_col[i];
                 a = av[i];
                 if (k < p.b_nrows) {
-                    bs = (I)p.b_rp[k];
-                    be = (I)p.b_rp[k + 1];
+                    const I r = (I)p.b_rp[k];
+                    if (f.split) {  // the chunk's part of the B row
+                        const uint32_t *sp = f.split + (uint64_t)k * f.nch1 + c0 / fr_chunk<Sem>();
+                        bs = r + (I)sp[0];
+                        be = r + (I)sp[1];
+                    } else {
+                        bs = r;
+                        be = (I)p.b_rp[k + 1];
+                    }
                 }
             }
             const int cnt = (int)min<uint64_t>((uint64_t)kWave, (uint64_t)(a1 - base));
@@ -324,7 +367,7 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
             // skip chunks with no product (mask granule 2^csh columns, a multiple of CH or the last)
             if (!((cm >> cap63(c0 >> f.csh)) & 1ull)) continue;
             const uint32_t c1 = (uint32_t)min<uint64_t>(p.ncols, c0 + CH);
-            fr_accumulate<Sem, I>(p, a0, a1, (uint32_t)c0, c1, acc, bits);
+            fr_accumulate<Sem, I>(f, a0, a1, (uint32_t)c0, c1, acc, bits);
             __syncthreads();
             // emit: thread t owns bitmap word t (32 columns); positions by a block scan
             uint32_t x = 0;
@@ -384,6 +427,8 @@ slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
     uint32_t csh = 14;
     while (csh < 63 && (a.ncols >> csh) > 63) ++csh;
     f.csh = csh;
+    f.split = nullptr;
+    f.nch1 = 0;
     SLAT_HIP(ctx, hipMemsetAsync(f.cnt, 0, 4, s));
     a.fr_mark = f.mark;
     f.a = a;
@@ -412,6 +457,12 @@ slat_status slat_fat_symbolic(slat_ctx *ctx, FatArgs &f, const Args &a, bool idx
     return SLAT_OK;
 }
 
+// split tables above this size are not built (the walks then filter B rows by column range)
+static const uint64_t kSplitBytes = [] {
+    const char *e = std::getenv("SLAT_FAT_SPLIT_BYTES");
+    return e ? std::strtoull(e, nullptr, 10) : (256ull << 20);
+}();
+
 template <typename Sem>
 static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
     const dim3 g((unsigned)ctx->cu_count);
@@ -419,6 +470,31 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
     // the chunk mask's granule must be a multiple of this instance's chunk
     FatArgs h = f;
     if ((1ull << h.csh) < fr_chunk<Sem>()) return hipErrorInvalidValue;
+    // B split by this instance's accumulator chunk, so each chunk's walk loads only its own entries
+    // (MAGNUS's column-chunk reordering, applied to B once instead of to every fat row's products)
+    const uint64_t nch = (h.a.ncols + fr_chunk<Sem>() - 1) / fr_chunk<Sem>();
+    const uint64_t nb = h.a.b_nrows;
+    uint32_t *split = nullptr;
+    h.split = nullptr;
+    h.nch1 = 0;
+    if (nch > 1 && nb * (nch + 1) * 4 <= kSplitBytes && !std::getenv("SLAT_NO_FAT_SPLIT")) {
+        if (slat_dev_alloc(ctx, (void **)&split, nb * (nch + 1) * 4, ctx->stream) == hipSuccess) {
+            const uint32_t sh = (uint32_t)__builtin_ctz(fr_chunk<Sem>());
+            const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb * (nch + 1) + kBlock - 1) / kBlock,
+                                                                                   (uint64_t)ctx->cu_count * 16));
+            hipLaunchKernelGGL(k_fr_splits, dim3(gs), dim3(kBlock), 0, ctx->stream, h.a.b_rp, h.a.b_col, nb,
+                               (uint32_t)(nch + 1), sh, split);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) {
+                slat_dev_free(ctx, split, ctx->stream);
+                return e;
+            }
+            h.split = split;
+            h.nch1 = (uint32_t)(nch + 1);
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     static std::atomic<uint64_t> attr{0};  // per device, as above
     if (!(attr.load(std::memory_order_relaxed) >> (ctx->device & 63) & 1)) {  // > 64 KB of dynamic LDS per block
         (void)hipFuncSetAttribute((const void *)k_fr_numeric<Sem, uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -429,7 +505,9 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
         hipLaunchKernelGGL((k_fr_numeric<Sem, uint32_t>), g, dim3(kFB), lds, ctx->stream, h);
     else
         hipLaunchKernelGGL((k_fr_numeric<Sem, uint64_t>), g, dim3(kFB), lds, ctx->stream, h);
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (split) slat_dev_free(ctx, split, ctx->stream);  // stream-ordered: reused only by later work
+    return e;
 }
 
 slat_status slat_fat_numeric(slat_ctx *ctx, FatArgs &f, const Args &a, int32_t dtype, bool f64any, bool idx32) {

@@ -14,6 +14,10 @@ struct FatArgs {
     uint8_t *mark;              // [n] 1 = fat
     unsigned long long *cmask;  // [list position] touched accumulator chunks (bit c: chunk c; 64 max)
     uint32_t csh;               // log2 of the chunk mask's granule (columns per mask bit)
+    // B split by accumulator chunk (numeric pass; null = none): split[k * nch1 + c] = the offset in B
+    // row k of its first entry with column >= c * chunk width (c = 0 .. nch1 - 1, the last = len)
+    const uint32_t *split;
+    uint32_t nch1;
 };
 }  // namespace slat
 

@@ -51,12 +51,6 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_PHASES
 #define SLAT_PHASES 0  // diagnostic builds: per-phase s_memtime cycles of k_numeric
 #endif
-#ifndef SLAT_SYM_PREFETCH
-#define SLAT_SYM_PREFETCH 0  // k_symbolic: load the next row's A segment ahead
-#endif
-#ifndef SLAT_PREFETCH
-#define SLAT_PREFETCH 0  // k_numeric: load the next row's A segment ahead (1 / 2: where, see k_numeric)
-#endif
 
 constexpr int kPhaseSlots = 16;  // [0..12] phases, [15] rows
 
@@ -900,18 +894,6 @@ struct RowWalker {
         single = nseg == 1;
         if (single) load_seg(a0);
     }
-    // a one-segment row whose A entries were loaded ahead (seg_loads into k0 / v0)
-    __device__ __forceinline__ RowWalker(const Args &p_, I a0_, I a1_, const uint32_t (&k0)[kRegQ], const S (&v0)[kRegQ])
-        : p(p_), a0(a0_), a1(a1_) {
-        len = (uint64_t)(a1 - a0);
-        nseg = 1;
-        single = true;
-        sfor<kRegQ>([&](auto Q) {
-            kq[Q] = k0[Q];
-            aq[Q] = v0[Q];
-        });
-        finish_seg();
-    }
     // the A entries [sb, min(a1, sb + kSeg)) of a row, kRegQ per lane (kSent / 0 past the end)
     __device__ static __forceinline__ void seg_loads(const Args &p, I sb, I a1, uint32_t *k, S *a) {
         const int lane = lane_id();
@@ -1245,41 +1227,10 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
-    // SLAT_SYM_PREFETCH (MODE 0 with the ELL copy): the next row's bounds and A segment are loaded
-    // once this row's bitmap walk is done, so the popcounts and stores overlap them
-    constexpr bool kPre = MODE == 0 && ELL && SLAT_SYM_PREFETCH != 0;
-    using SW = RowWalker<SemNone, I, ELL, false>;
-    I pa0 = 0, pa1 = 0;
-    uint32_t pk[kRegQ], pv[kRegQ];
-    bool pok = false;
-    auto prefetch = [&](uint64_t it2) {
-        pok = false;
-        if (it2 < nit) {
-            pa0 = (I)p.a_rp[it2];
-            pa1 = (I)p.a_rp[it2 + 1];
-            if (pa1 > pa0 && (uint64_t)(pa1 - pa0) <= SW::kSeg) {
-                SW::seg_loads(p, pa0, pa1, pk, pv);
-                pok = true;
-            }
-        }
-    };
-    if constexpr (kPre) prefetch((uint64_t)blockIdx.x * kWpb + wv);
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
-        bool pre_done = false;
-        auto pre_next = [&]() {
-            if constexpr (kPre)
-                if (!pre_done) {
-                    prefetch(it + stride);
-                    pre_done = true;
-                }
-        };
-        if (fat_row(p, row)) {  // the fat-row kernels' row
-            pre_next();
-            continue;
-        }
-        const bool have = kPre && pok;
-        const I a0 = kPre ? pa0 : (I)p.a_rp[row], a1 = kPre ? pa1 : (I)p.a_rp[row + 1];
+        if (fat_row(p, row)) continue;  // the fat-row kernels' row
+        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         if constexpr (MODE != 0) {
             if (!listed && sym_short_row((uint64_t)(a1 - a0), p.b_maxrow) != (MODE == 1)) continue;  // the other launch's row
         }
@@ -1298,7 +1249,7 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
                 wave_sync();
             }
         } else if (a1 > a0) {
-            SW rw = have ? SW(p, a0, a1, pk, pv) : SW(p, a0, a1);
+            RowWalker<SemNone, I, ELL, false> rw(p, a0, a1);
             uint64_t lo = 0, hi = p.ncols - 1;
             uint32_t cmask = 0xFFFFFFFFu;  // touched column chunks (MODE 2 only; else all)
             const uint32_t csh = MODE == 2 ? chunk_shift(p.ncols) : 0u;
@@ -1321,9 +1272,8 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
                 SymPass<1, Z> sp{BitmapPass<uint32_t, 1, Z>{L0, wlo, WIN}, p.stats != 0 && first};
                 if (!(p.ablate & 1u)) rw.template each_group<false>(sp);
                 wave_sync();
-                pre_next();
                 // count = popcount of the touched 64-word blocks only (word b*64 + lane per lane),
-                // which the same lanes then clear; four blocks' reads issued before any is used
+                // which the same lanes then clear
                 uint32_t lc = 0;
                 const uint32_t bmask = wave_or_u32(sp.bm.blk);
                 uint32_t *keep = nullptr;  // the stored bitmap of this row (Z launches with p.sbm)
@@ -1332,21 +1282,12 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
                         keep = p.sbm + row * ((uint64_t)p.nblk * kWave);
                         if (lane == 0) p.smask[row] = bmask;
                     }
-                uint32_t m = bmask;
-                while (m) {
-                    uint32_t ws[4], xs[4];
-                    sfor<4>([&](auto I_) {
-                        ws[I_] = m ? (uint32_t)__builtin_ctz(m) * kWave + lane : kSent;
-                        m &= m - 1;
-                    });
-                    sfor<4>([&](auto I_) { xs[I_] = ws[I_] != kSent ? L0[ws[I_]] : 0u; });
-                    sfor<4>([&](auto I_) {
-                        if (ws[I_] != kSent) {
-                            lc += __popc(xs[I_]);
-                            L0[ws[I_]] = 0;
-                            if (keep) keep[ws[I_]] = xs[I_];
-                        }
-                    });
+                for (uint32_t m = bmask; m; m &= m - 1) {
+                    const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
+                    const uint32_t x = L0[w];
+                    lc += __popc(x);
+                    L0[w] = 0;
+                    if (keep) keep[w] = x;
                 }
                 cnt += wave_sum_u32(lc);
                 if (first && p.stats) flops += wave_sum_u32(sp.nprod);
@@ -1361,7 +1302,6 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
                 for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) window(std::false_type{}, (uint32_t)wlo);
             }
         }
-        pre_next();  // rows without a bitmap walk (empty)
         if (lane == 0) p.counts[row] = cnt;
     }
     if (p.stats && lane == 0 && flops)
@@ -1437,43 +1377,11 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     uint64_t *ph = pc.ph;
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
-    // SLAT_PREFETCH (MODE 0 with the ELL copy): the next row's bounds and A segment are loaded while
-    // this row runs (1: after its word ranks, 2: after its accumulate pass), so a row does not start
-    // with the a_rp -> a_col load chain
-    constexpr int kPre = (MODE == 0 && ELL) ? SLAT_PREFETCH : 0;
     using RW = RowWalker<Sem, I, ELL, kVals>;
-    I pa0 = 0, pa1 = 0;
-    uint32_t pk[kRegQ];
-    S pv[kRegQ];
-    bool pok = false;  // pk / pv hold the segment of the row prefetched last
-    auto prefetch = [&](uint64_t it2) {
-        pok = false;
-        if (it2 < nit) {
-            pa0 = (I)p.a_rp[it2];
-            pa1 = (I)p.a_rp[it2 + 1];
-            if (pa1 > pa0 && (uint64_t)(pa1 - pa0) <= RW::kSeg) {
-                RW::seg_loads(p, pa0, pa1, pk, pv);
-                pok = true;
-            }
-        }
-    };
-    if constexpr (kPre != 0) prefetch((uint64_t)blockIdx.x * kWpb + wv);
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
-        bool pre_done = false;
-        auto pre_next = [&]() {
-            if constexpr (kPre != 0)
-                if (!pre_done) {
-                    prefetch(it + stride);
-                    pre_done = true;
-                }
-        };
-        if (fat_row(p, row)) {  // the fat-row kernels' row
-            pre_next();
-            continue;
-        }
-        const bool have = kPre != 0 && pok;
-        const I a0 = kPre != 0 ? pa0 : (I)p.a_rp[row], a1 = kPre != 0 ? pa1 : (I)p.a_rp[row + 1];
+        if (fat_row(p, row)) continue;  // the fat-row kernels' row
+        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         const uint64_t out_begin = p.c_rp[row], out_end = p.c_rp[row + 1];
         uint64_t out_pos = out_begin;
         uint32_t zeros = 0;
@@ -1540,7 +1448,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
             wave_sync();
             }
         } else if (a1 > a0) {
-            RW rw = have ? RW(p, a0, a1, pk, pv) : RW(p, a0, a1);
+            RW rw(p, a0, a1);
             const uint64_t len = rw.len;
             if constexpr (SLAT_PHASES) pin(rw.kq[0]);  // wait for the A entries inside phase 0
             mark(0);  // row bounds + A entries, group counts, tail compaction
@@ -1615,7 +1523,6 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                     if (wcnt == 0) return;  // bitmap empty: nothing to clear
                 }
                 mark(2);  // word ranks
-                if constexpr (kPre == 1) pre_next();
                 // narrow u32 slots when the row's sums provably stay below 2^32:
                 // max(A row) * max(B) * len(A row) < 2^32 (each output sums <= len products)
                 bool narrow = false;
@@ -1659,15 +1566,12 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                             });
                     } else if (!(p.ablate & 8u)) {
                         AccPass<Sem, NW, Z && R0, Z && R0, UNI> acc{W, vals, cols, p.ww, wlo, r0, nch, &pc};
-                        if constexpr (NW)
-                            rw.template each_group<true, SemU32Narrow, UNI>(acc, bv0);
-                        else
-                            rw.template each_group<true, Sem, UNI>(acc, bv0);
+                        using PS = std::conditional_t<NW, SemU32Narrow, Sem>;
+                        rw.template each_group<true, PS, UNI>(acc, bv0);
                     }
                     wave_sync();
                     if constexpr (SLAT_PHASES) (void)__builtin_amdgcn_readfirstlane((uint32_t)vals[0]);
                     mark(12);  // accumulate pass drain
-                    if constexpr (kPre == 2) pre_next();
                     // 4. emit at the row's slice, coalesced
                     // wave-uniform output base + 32-bit lane offsets
                     uint32_t *oc = p.c_col + out_pos;
@@ -1762,7 +1666,6 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 for (uint64_t wlo64 = lo & ~31ull; wlo64 <= hi; wlo64 += WIN) window(std::false_type{}, (uint32_t)wlo64);
             }
         }
-        pre_next();  // rows that returned early (empty, no outputs)
         mark(5);  // window clears, empty rows
         const uint32_t rz = p.ablate ? 0u : wave_sum_u32(zeros);  // ablation runs: no compaction
         const uint64_t got = out_pos - out_begin - rz;
@@ -2342,10 +2245,12 @@ template <typename Sem0, typename I>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_numeric_short(Args p) {
     numeric_short_body<Sem0, I>(p);
 }
-// u32: 6 waves per SIMD (6.6 KB of LDS per wave, <= 80 VGPRs; the wider semirings are held to 4
-// waves by their LDS anyway). Variant builds: -DSLAT_SHORT_WPE=w (0: no cap).
+// u32: 5 waves per SIMD (6.6 KB of LDS per wave, <= 96 VGPRs; the wider semirings are held to 4
+// waves by their LDS anyway). At 6 waves (<= 80 VGPRs) 28 VGPRs spilled to scratch and C4's numeric
+// pass took 1.235 ms against 0.942 ms here, 4 waves 1.053 ms (profiles/r03_ab_prefetch_short_wpe.txt).
+// Variant builds: -DSLAT_SHORT_WPE=w (0: no cap).
 #ifndef SLAT_SHORT_WPE
-#define SLAT_SHORT_WPE 6
+#define SLAT_SHORT_WPE 5
 #endif
 template <typename I>
 __global__ __launch_bounds__(kBlock)

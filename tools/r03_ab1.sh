@@ -13,3 +13,4 @@ SLAT_LIB_PATH=tools/var/libslat_wpe4.so timeout -k 10 300 python -u -m pytest te
 tail -n 2 $OUT/wpe4_tests.log
 SLAT_LIB_PATH=tools/var/libslat_wpe4.so timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu --no-c4 > $OUT/wpe4_bench.json 2> $OUT/wpe4_bench.err || { tail -30 $OUT/wpe4_bench.err; exit 1; }
 cat $OUT/wpe4_bench.json
+bash tools/r03_heavy.sh
