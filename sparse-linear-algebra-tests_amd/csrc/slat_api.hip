@@ -674,12 +674,21 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (num_lds > ctx->lds_per_block_max) return fail(ctx, SLAT_ENOTSUP, "LDS budget too small");
     const size_t sym_lds = (size_t)wpb * asym.ww * 4, sym_hash_lds = (size_t)wpb * kSymHashT * 4;
     const uint64_t row_blocks = (n + wpb - 1) / wpb;
-    const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * 16)));
+    // grid geometry knobs (A/B only): symbolic blocks per CU, numeric oversubscription factor
+    static const uint64_t kSymBpc = [] {
+        const char *e = std::getenv("SLAT_SYM_BPC");
+        return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 16ull;
+    }();
+    static const uint64_t kNumOver = [] {
+        const char *e = std::getenv("SLAT_NUM_OVER");
+        return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 1ull;
+    }();
+    const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * kSymBpc)));
     const int sem = dt == SLAT_U32 ? kSemU32 : dt == SLAT_SAT64 ? kSemSat64 : f64any ? kSemF64Any : kSemF64;
     const int hash_mode = batched ? 3 : 1;  // numeric instance of the short rows of a wide launch
     auto num_grid = [&](int mode, size_t lds) {
         const int nbpc = slat_numeric_blocks_per_cu(sem, mode, idx32, ell, lds);
-        return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc)));
+        return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc * kNumOver)));
     };
     const dim3 grid = num_grid(hash ? 2 : 0, num_lds);
     const dim3 hash_grid = hash ? num_grid(hash_mode, hash_lds) : dim3(1);
@@ -713,7 +722,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const uint64_t maxrow_a = A->max_row_nnz;
     const bool fat = !kNoFat && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
-    const size_t o_part = o_lc + lc_b, part_b = (ell && dt == SLAT_U32) ? 4096 * 8 : 0;
+    const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
     if ((st = slat_ensure_ws(ctx, o_fat + fat_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
@@ -722,11 +731,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         a.ell_col = (const uint32_t *)(ws + o_ecol);
         a.ell_val = ws + o_eval;
         a.ell_ng = ws + o_eng;
-        if (dt == SLAT_U32) {
+        if (dt != SLAT_F64) {  // u32 / Sat64: the clamped B-value summary for narrow slots
             a.b_vmax = ctx->d_vmax;
             a.epoch = ++ctx->epoch;
         }
-    } else if (dt == SLAT_U32 && kNarrowCsr) {
+    } else if (dt != SLAT_F64 && kNarrowCsr) {
         // B walked in CSR form: k_bvmax gives the numeric pass the same max(B) (narrow slots, and
         // hub rows accumulate in C instead of one re-traversal per rank chunk)
         a.b_vmax = ctx->d_vmax;
@@ -805,14 +814,19 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
                                             (unsigned long long *)(ws + o_part));
         else if (dt == SLAT_SAT64)
-            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
+            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
+                                                      (unsigned long long *)(ws + o_part));
         else
             be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
         SLAT_HIPC(be);
     } else if (a.b_vmax && B->nnz) {
         const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
-        hipLaunchKernelGGL(k_bvmax, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz, ctx->d_vmax,
-                           a.epoch);
+        if (dt == SLAT_U32)
+            hipLaunchKernelGGL(k_bvmax<uint32_t>, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz,
+                               ctx->d_vmax, a.epoch);
+        else
+            hipLaunchKernelGGL(k_bvmax<unsigned long long>, dim3(g), dim3(kBlock), 0, s,
+                               (const unsigned long long *)B->values, B->nnz, ctx->d_vmax, a.epoch);
         SLAT_HIPC(hipGetLastError());
     }
     slat::FatArgs fat_args = {};
@@ -854,8 +868,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
     }
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
-    // (u32 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
-    const bool bpart = ell && dt == SLAT_U32;
+    // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
+    const bool bpart = ell && dt != SLAT_F64;
     if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
                                bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
                                bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch)))

@@ -51,6 +51,9 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_PHASES
 #define SLAT_PHASES 0  // diagnostic builds: per-phase s_memtime cycles of k_numeric
 #endif
+#ifndef SLAT_SAT64_NARROW
+#define SLAT_SAT64_NARROW 1  // Sat64 rows under the u32 bound accumulate in u32 slots (variant builds: 0)
+#endif
 
 constexpr int kPhaseSlots = 16;  // [0..12] phases, [15] rows
 
@@ -142,7 +145,9 @@ struct SemSat64 {
     using V = unsigned long long;
     static constexpr int kSlots = 2;  // low / high 32-bit halves of the products, summed apart
     static constexpr bool kOrdered = false;
-    static constexpr bool kNarrowable = false;
+    // u32 slots when a row cannot reach 2^32 (the same bound as u32: every product and sum is exact
+    // in 32 bits, so no saturation can happen): 6 B per output slot instead of 18 B
+    static constexpr bool kNarrowable = SLAT_SAT64_NARROW;
     __device__ static __forceinline__ P prod(S a, S b) {
         return __umul64hi(a, b) != 0 ? ~0ull : a * b;  // Saturating<u64> product
     }
@@ -265,6 +270,15 @@ __device__ __forceinline__ S readlane_val(S v, int l) {
     }
 }
 
+// a value clamped to u32 (the narrow-slot bound's inputs: a u64 value >= 2^32 never passes it)
+template <typename S>
+__device__ __forceinline__ uint32_t sat32(S v) {
+    if constexpr (sizeof(S) == 4)
+        return (uint32_t)v;
+    else
+        return (uint64_t)v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)v;
+}
+
 // Ordered traversal (f64): A's row entries in order, lanes spread over one B row (distinct
 // columns), 64 A entries' row pointers prefetched at a time. The first 64 elements of the B rows
 // of kOrdAhead consecutive entries are loaded before any of them is visited, so the visits (in A
@@ -344,10 +358,10 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
             const uint64_t u = (uint64_t)t * 4 + e;
             c[e] = u < len ? col[s0 + u] : kSent;
             v[e] = u < len ? val[s0 + u] : S(0);
-            if constexpr (std::is_same<S, uint32_t>::value)
+            if constexpr (!std::is_floating_point<S>::value)
                 if (u < len) {
-                    mx = max(mx, (uint32_t)v[e]);
-                    mn = min(mn, (uint32_t)v[e]);
+                    mx = max(mx, sat32(v[e]));
+                    mn = min(mn, sat32(v[e]));
                 }
         }
         ((uint4 *)ecol)[g] = make_uint4(c[0], c[1], c[2], c[3]);
@@ -359,8 +373,8 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
             for (int e = 0; e < 4; ++e) eval[(uint64_t)g * 4 + e] = v[e];
         }
     }
-    if constexpr (std::is_same<S, uint32_t>::value) {
-        // max and min B value of this block, stored as one partial ((~min << 32) | max) that
+    if constexpr (!std::is_floating_point<S>::value) {
+        // max and min B value of this block (clamped to u32), stored as one partial ((~min << 32) | max) that
         // k_scan_rows reduces into the epoch-tagged words: no same-address atomics and no
         // round trip at the end of every block
         __shared__ uint32_t bm[kBlock / kWave], bn[kBlock / kWave];
@@ -383,12 +397,12 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
 
 // the same B-value summary when B is walked in CSR form (no ELL copy): max and ~min of the u32
 // values, epoch-tagged, one atomic pair per block
-static __global__ __launch_bounds__(kBlock) void k_bvmax(const uint32_t *val, uint64_t nnz,
-                                                          unsigned long long *vmax, uint32_t epoch) {
+template <typename S>
+__global__ __launch_bounds__(kBlock) void k_bvmax(const S *val, uint64_t nnz, unsigned long long *vmax, uint32_t epoch) {
     uint32_t mx = 0, mn = 0xFFFFFFFFu;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nnz; i += (uint64_t)gridDim.x * kBlock) {
-        mx = max(mx, val[i]);
-        mn = min(mn, val[i]);
+        mx = max(mx, sat32(val[i]));
+        mn = min(mn, sat32(val[i]));
     }
     __shared__ uint32_t bm[kBlock / kWave], bn[kBlock / kWave];
     mx = wave_max_u32(mx);
@@ -471,12 +485,15 @@ __device__ __forceinline__ Quad<typename Sem::S> prods(typename Sem::S a, const 
     return pr;
 }
 
-// u32 products of a row whose bound max(A) * max(B) * len < 2^32 holds: no clamp needed
-struct SemU32Narrow {
-    using S = uint32_t;
+// products of a row whose bound max(A) * max(B) * len < 2^32 holds (u32 or Sat64 values): exact in
+// 32 bits, no clamp needed
+template <typename ST>
+struct SemNarrowT {
+    using S = ST;
     static constexpr bool kNarrowable = true;
-    __device__ static __forceinline__ S prod(S a, S b) { return a * b; }
+    __device__ static __forceinline__ S prod(S a, S b) { return (S)((uint32_t)a * (uint32_t)b); }
 };
+using SemU32Narrow = SemNarrowT<uint32_t>;
 
 // passes that need no values (symbolic, bitmap, column span) walk with this stand-in semiring
 struct SemNone {
@@ -924,7 +941,7 @@ struct RowWalker {
         const int lane = lane_id();
         sfor<kRegQ>([&](auto Q) {
             if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
-            if constexpr (Sem::kNarrowable) amax = max(amax, (uint32_t)aq[Q]);
+            if constexpr (Sem::kNarrowable) amax = max(amax, sat32(aq[Q]));
         });
         if constexpr (!ELL) return;
         uint32_t mx = 0;
@@ -1204,6 +1221,89 @@ __host__ __device__ constexpr bool sym_short_row(uint64_t len, uint32_t b_maxrow
     return len * b_maxrow <= kSymHashT * 7 / 10;
 }
 
+// The structural nnz of one output row (symbolic, one wavefront; MODE as in k_symbolic), or kNoRow
+// when the row belongs to the other launch of its category. L0: the wave's LDS words (zero / kSent).
+constexpr uint64_t kNoRow = ~0ull;
+template <typename I, bool ELL, int MODE>
+__device__ __forceinline__ uint64_t sym_row(const Args &p, uint64_t row, bool listed, uint32_t *L0,
+                                            unsigned long long &flops) {
+    const int lane = lane_id();
+    const uint32_t WIN = p.ww * 32;
+    const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
+    if constexpr (MODE != 0) {
+        if (!listed && sym_short_row((uint64_t)(a1 - a0), p.b_maxrow) != (MODE == 1)) return kNoRow;  // the other launch's row
+    }
+    uint64_t cnt = 0;
+    if constexpr (MODE == 1) {
+        if (a1 > a0) {
+            // short row: distinct columns = keys inserted into the wave's hash table
+            RowWalker<SemNone, I, ELL, false> rw(p, a0, a1);
+            HashCount hc{L0};
+            rw.template each_group<false>(hc);
+            wave_sync();
+            cnt = wave_sum_u32(hc.cnt);
+            if (p.stats) flops += wave_sum_u32(hc.nprod);
+            uint4 *k4 = (uint4 *)L0;
+            for (uint32_t w = lane; w < kSymHashT / 4; w += kWave) k4[w] = make_uint4(kSent, kSent, kSent, kSent);
+            wave_sync();
+        }
+    } else if (a1 > a0) {
+        RowWalker<SemNone, I, ELL, false> rw(p, a0, a1);
+        uint64_t lo = 0, hi = p.ncols - 1;
+        uint32_t cmask = 0xFFFFFFFFu;  // touched column chunks (MODE 2 only; else all)
+        const uint32_t csh = MODE == 2 ? chunk_shift(p.ncols) : 0u;
+        if (p.wide) {
+            SpanPass<uint32_t, MODE == 2> mm{csh};
+            rw.template each_group<false>(mm);
+            const uint32_t l = wave_min_u32(mm.l), h = wave_max_u32(mm.h);
+            if constexpr (MODE == 2) cmask = wave_or_u32(mm.cm);
+            lo = l;
+            hi = h;
+            if (l > h) {
+                lo = 1;
+                hi = 0;
+            }
+        }
+        bool first = true;
+        // one window; Z (std::true_type) when it starts at column 0 and covers every column
+        auto window = [&](auto ztag, uint32_t wlo) {
+            constexpr bool Z = decltype(ztag)::value;
+            SymPass<1, Z> sp{BitmapPass<uint32_t, 1, Z>{L0, wlo, WIN}, p.stats != 0 && first};
+            if (!(p.ablate & 1u)) rw.template each_group<false>(sp);
+            wave_sync();
+            // count = popcount of the touched 64-word blocks only (word b*64 + lane per lane),
+            // which the same lanes then clear
+            uint32_t lc = 0;
+            const uint32_t bmask = wave_or_u32(sp.bm.blk);
+            uint32_t *keep = nullptr;  // the stored bitmap of this row (Z launches with p.sbm)
+            if constexpr (Z)
+                if (p.sbm) {
+                    keep = p.sbm + row * ((uint64_t)p.nblk * kWave);
+                    if (lane == 0) p.smask[row] = bmask;
+                }
+            for (uint32_t m = bmask; m; m &= m - 1) {
+                const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
+                const uint32_t x = L0[w];
+                lc += __popc(x);
+                L0[w] = 0;
+                if (keep) keep[w] = x;
+            }
+            cnt += wave_sum_u32(lc);
+            if (first && p.stats) flops += wave_sum_u32(sp.nprod);
+            first = false;
+            wave_sync();
+        };
+        if (!p.wide) {
+            window(std::true_type{}, 0u);
+        } else if constexpr (MODE == 2) {
+            for_windows(lo, hi, WIN, cmask, csh, [&](uint32_t wlo) { window(std::false_type{}, wlo); });
+        } else {
+            for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) window(std::false_type{}, (uint32_t)wlo);
+        }
+    }
+    return cnt;
+}
+
 template <typename I, bool ELL, int MODE = 0>
 __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -1222,7 +1322,6 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     }
     for (uint32_t w = lane; w < region_w; w += kWave) L0[w] = MODE == 1 ? kSent : 0u;
     wave_sync();
-    const uint32_t WIN = p.ww * 32;
     unsigned long long flops = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
@@ -1230,106 +1329,38 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
         if (fat_row(p, row)) continue;  // the fat-row kernels' row
-        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
-        if constexpr (MODE != 0) {
-            if (!listed && sym_short_row((uint64_t)(a1 - a0), p.b_maxrow) != (MODE == 1)) continue;  // the other launch's row
-        }
-        uint64_t cnt = 0;
-        if constexpr (MODE == 1) {
-            if (a1 > a0) {
-                // short row: distinct columns = keys inserted into the wave's hash table
-                RowWalker<SemNone, I, ELL, false> rw(p, a0, a1);
-                HashCount hc{L0};
-                rw.template each_group<false>(hc);
-                wave_sync();
-                cnt = wave_sum_u32(hc.cnt);
-                if (p.stats) flops += wave_sum_u32(hc.nprod);
-                uint4 *k4 = (uint4 *)L0;
-                for (uint32_t w = lane; w < kSymHashT / 4; w += kWave) k4[w] = make_uint4(kSent, kSent, kSent, kSent);
-                wave_sync();
-            }
-        } else if (a1 > a0) {
-            RowWalker<SemNone, I, ELL, false> rw(p, a0, a1);
-            uint64_t lo = 0, hi = p.ncols - 1;
-            uint32_t cmask = 0xFFFFFFFFu;  // touched column chunks (MODE 2 only; else all)
-            const uint32_t csh = MODE == 2 ? chunk_shift(p.ncols) : 0u;
-            if (p.wide) {
-                SpanPass<uint32_t, MODE == 2> mm{csh};
-                rw.template each_group<false>(mm);
-                const uint32_t l = wave_min_u32(mm.l), h = wave_max_u32(mm.h);
-                if constexpr (MODE == 2) cmask = wave_or_u32(mm.cm);
-                lo = l;
-                hi = h;
-                if (l > h) {
-                    lo = 1;
-                    hi = 0;
-                }
-            }
-            bool first = true;
-            // one window; Z (std::true_type) when it starts at column 0 and covers every column
-            auto window = [&](auto ztag, uint32_t wlo) {
-                constexpr bool Z = decltype(ztag)::value;
-                SymPass<1, Z> sp{BitmapPass<uint32_t, 1, Z>{L0, wlo, WIN}, p.stats != 0 && first};
-                if (!(p.ablate & 1u)) rw.template each_group<false>(sp);
-                wave_sync();
-                // count = popcount of the touched 64-word blocks only (word b*64 + lane per lane),
-                // which the same lanes then clear
-                uint32_t lc = 0;
-                const uint32_t bmask = wave_or_u32(sp.bm.blk);
-                uint32_t *keep = nullptr;  // the stored bitmap of this row (Z launches with p.sbm)
-                if constexpr (Z)
-                    if (p.sbm) {
-                        keep = p.sbm + row * ((uint64_t)p.nblk * kWave);
-                        if (lane == 0) p.smask[row] = bmask;
-                    }
-                for (uint32_t m = bmask; m; m &= m - 1) {
-                    const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
-                    const uint32_t x = L0[w];
-                    lc += __popc(x);
-                    L0[w] = 0;
-                    if (keep) keep[w] = x;
-                }
-                cnt += wave_sum_u32(lc);
-                if (first && p.stats) flops += wave_sum_u32(sp.nprod);
-                first = false;
-                wave_sync();
-            };
-            if (!p.wide) {
-                window(std::true_type{}, 0u);
-            } else if constexpr (MODE == 2) {
-                for_windows(lo, hi, WIN, cmask, csh, [&](uint32_t wlo) { window(std::false_type{}, wlo); });
-            } else {
-                for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) window(std::false_type{}, (uint32_t)wlo);
-            }
-        }
+        const uint64_t cnt = sym_row<I, ELL, MODE>(p, row, listed, L0, flops);
+        if (cnt == kNoRow) continue;
         if (lane == 0) p.counts[row] = cnt;
     }
     if (p.stats && lane == 0 && flops)
         atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
 }
 
-// variant builds: -DSLAT_NUM_WPE=w caps k_numeric's registers for w waves per SIMD
-#ifndef SLAT_NUM_ATTR
-#ifdef SLAT_NUM_WPE
+// k_numeric's register cap: 3 waves per SIMD (<= 168 VGPRs). The wide-slot (Sat64 / f64) and
+// narrow instances spill nothing at that cap and gain the third wave: Sat64 A^6*A numeric
+// 146 -> 117 us, u32 unchanged (profiles/r03_ab_sat64_narrow.txt, variant "w3"). At 4 waves (128
+// VGPRs) round 2 saw a memory fault; it came from that build's uncommitted compacted-bitmap code,
+// not from the cap. Variant builds: -DSLAT_NUM_WPE=w.
+#ifndef SLAT_NUM_WPE
+#define SLAT_NUM_WPE 3
+#endif
 #define SLAT_NUM_ATTR __attribute__((amdgpu_waves_per_eu(SLAT_NUM_WPE)))
-#else
-#define SLAT_NUM_ATTR
-#endif
-#endif
 
 // MODE 0: every row by bitmap windows. Wide launches split the rows by output count (known from
 // symbolic): MODE 1 accumulates the rows with <= kHashT / 2 outputs in the LDS hash table and
 // skips the rest, MODE 2 takes the rest by row-span windows.
-template <typename Sem, typename I, bool ELL, int MODE = 0>
-__global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
+// The numeric pass of one wavefront over rows first, first + stride, ... (k_numeric: the grid's
+// waves; k_tiny: the waves of its one workgroup). smem8: the workgroup's LDS, wave wv's region at
+// wv * its size.
+template <typename Sem, typename I, bool ELL, int MODE>
+__device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int wv, uint64_t first, uint64_t stride) {
     using S = typename Sem::S;
     using V = typename Sem::V;
     constexpr int kWpb = kBlock / kWave;
     constexpr bool kVals = !Sem::kOrdered;  // f64 accumulates from an ordered CSR walk
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
 
     const int lane = lane_id();
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
     const NumLayout lay = num_layout(p.ww, p.area);
     // per-wave region: the bitmap window + rank slots, or (wide launches) the hash table in the
     // same place
@@ -1348,7 +1379,9 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
             const unsigned long long vi = ((volatile unsigned long long *)p.b_vmax)[kVMinInvWord];
             if ((uint32_t)(v >> 32) == p.epoch) {
                 bvmax = (uint32_t)v;
-                buni = (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax;
+                // (a wider value type clamps to u32 in the summary: all-equal clamped values are
+                // not a pattern unless below the clamp)
+                buni = (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax && (sizeof(S) == 4 || bvmax != 0xFFFFFFFFu);
             }
         }
     const S bv0 = (S)bvmax;
@@ -1370,7 +1403,6 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
 
     const uint32_t WIN = p.ww * 32;
     uint32_t zrows = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     PhaseClock pc{};
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
     auto mark = [&](int i) { pc.mark(i); };
@@ -1378,7 +1410,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     using RW = RowWalker<Sem, I, ELL, kVals>;
-    for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
+    for (uint64_t it = first; it < nit; it += stride) {
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
         if (fat_row(p, row)) continue;  // the fat-row kernels' row
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
@@ -1527,14 +1559,14 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                 // max(A row) * max(B) * len(A row) < 2^32 (each output sums <= len products)
                 bool narrow = false;
                 if constexpr (Sem::kNarrowable) {
-                    // (rw.amax covers the row once its segments went through load_seg: always
-                    // with ELL and for one-segment rows; a longer row in the CSR walk reads its A
-                    // values once more here)
+                    // (rw.amax covers a one-segment row; a longer row reads its A values once more
+                    // here: with a stored bitmap nothing walked its later segments yet, so its
+                    // amax would hold nothing)
                     if (bvmax != 0xFFFFFFFFu) {
                         uint32_t am = rw.amax;
-                        if (!ELL && !rw.single) {
-                            const uint32_t *av = (const uint32_t *)p.a_val;
-                            for (I j = a0 + (I)lane; j < a1; j += (I)kWave) am = max(am, av[j]);
+                        if (!rw.single) {
+                            const S *av = (const S *)p.a_val;
+                            for (I j = a0 + (I)lane; j < a1; j += (I)kWave) am = max(am, sat32(av[j]));
                         }
                         const uint64_t x = (uint64_t)wave_max_u32(am) * bvmax;
                         narrow = x == 0 || len <= 0xFFFFFFFFull / x;
@@ -1566,7 +1598,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                             });
                     } else if (!(p.ablate & 8u)) {
                         AccPass<Sem, NW, Z && R0, Z && R0, UNI> acc{W, vals, cols, p.ww, wlo, r0, nch, &pc};
-                        using PS = std::conditional_t<NW, SemU32Narrow, Sem>;
+                        using PS = std::conditional_t<NW, SemNarrowT<S>, Sem>;
                         rw.template each_group<true, PS, UNI>(acc, bv0);
                     }
                     wave_sync();
@@ -1605,8 +1637,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                     // u32 rows under the narrow bound cannot overflow a u32 sum, so their atomics
                     // in C are exact too: no re-traversal per rank chunk for hub rows (B walked in
                     // CSR form; the ELL instances keep their registers: +3 us on the 30^3 bench)
-                    constexpr bool kGO =
-                        GlobalOverflow<Sem>::value || (std::is_same<Sem, SemU32>::value && NW && !ELL);
+                    constexpr bool kGO = GlobalOverflow<Sem>::value || (Sem::kNarrowable && NW && !ELL);
                     if constexpr (kGO) {
                         if (wcnt > cap) {
                             // one pass into the C slice: zero it, then global atomics at out + rank
@@ -1618,7 +1649,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
                             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                             GlobalAcc<Sem> ga{W, p.ww, Z ? 0u : wlo, lim, oc, ov};
                             if constexpr (NW)
-                                rw.template each_group<true, SemU32Narrow, decltype(uni_tag)::value>(ga, bv0);
+                                rw.template each_group<true, SemNarrowT<S>, decltype(uni_tag)::value>(ga, bv0);
                             else
                                 rw.template each_group<true>(ga);
                             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
@@ -1682,6 +1713,14 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     // rows that lost explicit zeros (rare): counted straight into the mapped host word
     if (lane == 0 && zrows)
         __hip_atomic_fetch_add(&p.host_out[2], (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename Sem, typename I, bool ELL, int MODE = 0>
+__global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
+    constexpr int kWpb = kBlock / kWave;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
+    numeric_rows<Sem, I, ELL, MODE>(p, smem8, wv, (uint64_t)blockIdx.x * kWpb + wv, (uint64_t)gridDim.x * kWpb);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2094,7 +2133,9 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
             const unsigned long long vi = ((volatile unsigned long long *)p.b_vmax)[kVMinInvWord];
             if ((uint32_t)(v >> 32) == p.epoch) {
                 bvmax = (uint32_t)v;
-                buni = (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax;
+                // (a wider value type clamps to u32 in the summary: all-equal clamped values are
+                // not a pattern unless below the clamp)
+                buni = (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax && (sizeof(S) == 4 || bvmax != 0xFFFFFFFFu);
             }
         }
     const S bv0 = (S)bvmax;
@@ -2277,6 +2318,37 @@ constexpr int kScanThreads = SLAT_SCAN_THREADS, kScanItems = SLAT_SCAN_ITEMS;
 constexpr uint64_t kScanTile = (uint64_t)kScanThreads * kScanItems;
 constexpr unsigned long long kStAgg = 1ull << 40, kStInc = 2ull << 40, kStVal = (1ull << 40) - 1;
 
+// One lane: publish tile `tile`'s aggregate, walk back over the earlier tiles' status words (tags of
+// this epoch: an aggregate, or an inclusive prefix that ends the walk) and publish the tile's own
+// inclusive prefix; returns its exclusive prefix. Tiles are taken in ticket order, so every earlier
+// tile belongs to a block that is running or done and never waits on a later one.
+__device__ __forceinline__ unsigned long long lookback_prefix(unsigned long long *status, uint64_t tile, uint32_t epoch,
+                                                              unsigned long long agg) {
+    auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto st = [](unsigned long long *x, unsigned long long v) {
+        __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    const unsigned long long tag = (unsigned long long)epoch << 42;
+    unsigned long long excl = 0;
+    if (tile == 0) {
+        st(&status[0], tag | kStInc | agg);
+        return 0;
+    }
+    st(&status[tile], tag | kStAgg | agg);
+    for (uint64_t j = tile - 1;; --j) {
+        unsigned long long x;
+        while (true) {
+            x = ld(&status[j]);
+            if ((x >> 42) == epoch && (x & (kStAgg | kStInc)) != 0) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        excl += x & kStVal;
+        if (x & kStInc) break;
+    }
+    st(&status[tile], tag | kStInc | (excl + agg));
+    return excl;
+}
+
 __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long long v) {
     const int lane = lane_id();
 #pragma unroll
@@ -2337,21 +2409,7 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
         // max row first (its result waited for), then the status: the max is in place once any
         // later tile sees this tile's status
         pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
-        unsigned long long excl = 0;
-        if (tile == 0) {
-            st(&status[0], tag | kStInc | agg);
-        } else {
-            st(&status[tile], tag | kStAgg | agg);
-            for (uint64_t j = tile - 1;; --j) {
-                unsigned long long x;
-                do {
-                    x = ld(&status[j]);
-                } while ((x >> 42) != epoch || (x & (kStAgg | kStInc)) == 0);
-                excl += x & kStVal;
-                if (x & kStInc) break;
-            }
-            st(&status[tile], tag | kStInc | (excl + agg));
-        }
+        const unsigned long long excl = lookback_prefix(status, tile, epoch, agg);
         s_bcast[1] = excl;
         if (tile == ntiles - 1) {
             if (n > 0) rp[0] = 0;

@@ -360,3 +360,29 @@ def test_matmul_progress_lines(ctx, capfd):
     assert c.nnz() > 0
     a.matmul_par(a)
     assert "symbolic:" not in capfd.readouterr().err  # off again
+
+
+@pytest.mark.parametrize("dtype", [slat.U32, slat.SAT64])
+@pytest.mark.parametrize("vbig", [1 << 12, 1 << 20, (1 << 31) + 5])
+def test_long_rows_narrow_bound_stored_bitmap(ctx, dtype, vbig):
+    """Rows of more than one A segment (> 256 entries) in a single-window launch, whose stored
+    bitmap means numeric never walked their later segments before choosing the slot width: the
+    narrow (u32-slot) bound must still see every A value. Large values in the later segments make
+    the exact sums pass 2^32 (u32 saturates, Sat64 keeps them)."""
+    rng = np.random.default_rng(31)
+    n = 3000
+    rows, cols, vals = [], [], []
+    for r in range(0, n, 7):  # rows of 300..700 entries, the big values only past entry 256
+        k = int(rng.integers(300, 700))
+        c = np.sort(rng.choice(n, k, replace=False))
+        v = np.ones(k, np.uint64)
+        v[260:] = rng.integers(1, vbig, k - 260)
+        rows.append(np.full(k, r)), cols.append(c), vals.append(v)
+    for r in range(n):  # B-side rows for every column: short, value 3
+        rows.append(np.array([r, r])), cols.append(np.array([r, (r * 7 + 1) % n])), vals.append(np.full(2, 3, np.uint64))
+    R, Cc, Vv = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
+    key = R.astype(np.int64) * n + Cc
+    _, first = np.unique(key, return_index=True)
+    R, Cc, Vv = R[first], Cc[first], Vv[first]
+    a = O.from_coo(n, R, Cc, Vv.astype(np.uint32) if dtype == slat.U32 else Vv, DT[dtype])
+    assert_same(to_dev(a, dtype)._spgemm(to_dev(a, dtype)), O.matmul_seq(a, a), f"long rows vbig={vbig}")

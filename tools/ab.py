@@ -19,7 +19,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(c4: bool, steps: int, only_c4: bool = False):
+def child(c4: bool, steps: int, only_c4: bool = False, sat64: bool = False):
     sys.path.insert(0, os.path.join(ROOT, "sparse-linear-algebra-tests_amd"))
     import numpy as np
 
@@ -27,9 +27,12 @@ def child(c4: bool, steps: int, only_c4: bool = False):
     ctx = slat.Context(0)
     out = {}
     legs = ([] if only_c4 else [("a7", 30, 7, steps)]) + ([("c4", 100, 4, max(10, steps // 10))] if c4 or only_c4 else [])
+    legs += [("s7", 30, 7, steps)] if sat64 else []
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
     for name, side, power, k in legs:
         A = slat.torus_thinned_device(side, 3.0, slat.StdRng(), ctx)
+        if name == "s7":  # MagnusMatrix (Sat64) on the same torus
+            A = slat.MagnusMatrix.from_host(A.host().astype(slat.SAT64), ctx)
         P = A
         for _ in range(2, power):
             P = P.matmul(A)
@@ -63,10 +66,11 @@ def main():
     ap.add_argument("--c4", action="store_true")
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--only-c4", action="store_true", help="child: the C4 leg alone")
+    ap.add_argument("--sat64", action="store_true", help="add the Sat64 (MagnusMatrix) A^6*A leg")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     if a.child:
-        child(a.c4, a.steps, a.only_c4)
+        child(a.c4, a.steps, a.only_c4, a.sat64)
         return
     res = {}
     for r in range(a.reps):
@@ -80,7 +84,8 @@ def main():
             for kv in filter(None, knobs.split(",")):
                 k, _, val = kv.partition("=")
                 env[k] = val
-            cmd = [sys.executable, os.path.abspath(__file__), "--child", "--steps", str(a.steps)] + (["--c4"] if a.c4 else [])
+            cmd = ([sys.executable, os.path.abspath(__file__), "--child", "--steps", str(a.steps)] + (["--c4"] if a.c4 else [])
+                   + (["--sat64"] if a.sat64 else []))
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
                 print(f"{v}: FAILED rc={p.returncode}\n{p.stderr[-3000:]}", flush=True)
