@@ -233,6 +233,7 @@ hipError_t slat_dev_alloc(slat_ctx *ctx, void **p, size_t bytes, hipStream_t s) 
     if (e == hipSuccess) {
         ctx->live[*p] = {*p, r, s, *p};
         ctx->chunks[*p] = r;
+        ctx->mem_changed = true;
     }
     return e;
 }
@@ -251,6 +252,7 @@ void slat_dev_free(slat_ctx *ctx, void *p, hipStream_t s) {
                 ctx->cache_bytes -= ctx->cache[i].bytes;
                 ctx->chunks.erase(ctx->cache[i].p);
                 (void)hipFree(ctx->cache[i].p);
+                ctx->mem_changed = true;
                 ctx->cache.erase(ctx->cache.begin() + (std::ptrdiff_t)i);
             } else {
                 ++i;
@@ -279,6 +281,7 @@ void slat_dev_trim(slat_ctx *ctx) {
             ctx->cache_bytes -= ctx->cache[i].bytes;
             ctx->chunks.erase(ctx->cache[i].p);
             (void)hipFree(ctx->cache[i].p);
+            ctx->mem_changed = true;
             ctx->cache.erase(ctx->cache.begin() + (std::ptrdiff_t)i);
         } else {
             ++i;  // part of a chunk that still holds live pieces
@@ -504,13 +507,18 @@ __global__ void k_signal(unsigned long long *word, unsigned long long v) {
 // Every 2^16 polls the stream is queried, so a faulted kernel surfaces as an error, not a hang.
 // SLAT_WAIT=sync | query selects the other two, SLAT_WAIT=write stores the word with
 // hipStreamWriteValue64 instead of k_signal (A/B only).
-static hipError_t wait_stream(slat_ctx *ctx, hipStream_t s) {
+static int wait_mode() {
     static const int mode = [] {
         const char *e = std::getenv("SLAT_WAIT");
         if (std::getenv("SLAT_BLOCKING_SYNC") || (e && !std::strcmp(e, "sync"))) return 1;
         if (e && !std::strcmp(e, "write")) return 3;  // the sequence word stored by a stream write op
         return e && !std::strcmp(e, "query") ? 2 : 0;
     }();
+    return mode;
+}
+// signalled != 0: the call's last kernel stores that sequence number itself (signal_done)
+static hipError_t wait_stream(slat_ctx *ctx, hipStream_t s, unsigned long long signalled = 0) {
+    const int mode = wait_mode();
     hipError_t e;
     if (mode == 1) return hipStreamSynchronize(s);
     if (mode == 2) {
@@ -518,8 +526,9 @@ static hipError_t wait_stream(slat_ctx *ctx, hipStream_t s) {
         }
         return e;
     }
-    const unsigned long long seq = ++ctx->done_seq;
-    if (mode == 3) {
+    const unsigned long long seq = signalled ? signalled : ++ctx->done_seq;
+    if (signalled) {
+    } else if (mode == 3) {
         if ((e = hipStreamWriteValue64(s, ctx->h_out_dev + 7, seq, 0)) != hipSuccess) return e;
     } else {
         hipLaunchKernelGGL(k_signal, dim3(1), dim3(1), 0, s, ctx->h_out_dev + 7, seq);
@@ -626,8 +635,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
 
     // 32-bit offsets whenever every position fits (the common case; halves the index math)
     const bool idx32 = A->nnz < 0xFFFFFFFFull && B->nnz < 0xFFFFFFFFull && !(flags & SLAT_FLAG_IDX64);
-    uint32_t ablate = 0;  // experiments only: never reaches the real pipeline's kernels
-    if (const char *e_ = std::getenv("SLAT_ABLATE")) ablate = (uint32_t)std::atoi(e_);
+    // environment knobs (A/B experiments only) are read once: a getenv per call is host time on
+    // every call
+    static const uint32_t ablate = [] {  // experiments only: never reaches the real pipeline's kernels
+        const char *e = std::getenv("SLAT_ABLATE");
+        return e ? (uint32_t)std::atoi(e) : 0u;
+    }();
     Args asym = a;
     pick_window(ncols, kWave, 1984, asym.ww, asym.wide);
     pick_window(ncols, kWave, 1984, a.ww, a.wide);
@@ -638,7 +651,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // Wide launches (columns beyond one window) split the rows by MAGNUS-style category into two
     // launches per pass: short rows in a per-wave LDS hash table (mode 1), the rest by row-span
     // windows (mode 2; numeric windows of 1024 words keep two blocks per CU).
-    const bool hash = asym.wide && !std::getenv("SLAT_NO_HASH");
+    static const bool kNoHash = std::getenv("SLAT_NO_HASH") != nullptr;
+    const bool hash = asym.wide && !kNoHash;
     if (hash) {
         a.ww = std::min<uint32_t>(a.ww, 1024);
         a.b_maxrow = asym.b_maxrow = (uint32_t)std::min<uint64_t>(maxrow_b, 0xFFFFFFFFull);
@@ -646,20 +660,34 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // padded ELL copy of B when its rows are short (bounded blow-up)
     const uint64_t wq = (maxrow_b + 3) / 4;
     const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
+    // small products: the whole call in one kernel (slat_tiny.hip) — one window of at most 8192
+    // columns, 32-bit offsets, a product bound that a wave per row finishes in microseconds, and no
+    // per-pass timing or stats (those report the regular pipeline's passes)
+    static const bool kNoTiny = std::getenv("SLAT_NO_TINY") != nullptr;
+    const bool tiny = !kNoTiny && !asym.wide && ncols <= 8192 && n <= 4096 && idx32 && wait_mode() == 0 &&
+                      !(flags & (SLAT_FLAG_TIMING | SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) &&
+                      g_progress.load(std::memory_order_relaxed) == 0 &&
+                      (unsigned __int128)a_nnz_block * maxrow_b <= (1u << 18);
+    static const bool kNoEll = std::getenv("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
-                     !std::getenv("SLAT_NO_ELL");  // 24-bit row index, 31-bit byte offsets in the kernels
+                     !kNoEll && !tiny;  // 24-bit row index, 31-bit byte offsets in the kernels
 
     // LDS sizing and grids. The numeric grid is the kernel's resident capacity (waves stride over
     // rows; measured faster than oversubscribing); symbolic takes up to 16 blocks per CU.
     const int wpb = kBlock / kWave;
-    if (const char *e_ = std::getenv("SLAT_CAP")) a.area = 6 * std::max(64, std::atoi(e_));  // tuning knob
+    static const int kCap = [] {  // tuning knob: rank slots per wave
+        const char *e = std::getenv("SLAT_CAP");
+        return e ? std::max(64, std::atoi(e)) : 0;
+    }();
+    if (kCap) a.area = 6 * kCap;
     a.area = (a.area + 15) & ~15u;
     const size_t num_lds = (size_t)wpb * num_layout(a.ww, a.area).bytes;
     // short rows batched several per hash table (integer semirings with the ELL copy of B), else
     // one row per table; composite (row, column) keys need the column bits + 6 <= 31
     // symbolic batches for every value type (it never reads values); numeric for the integer ones
-    const bool sym_batched = hash && ell && !std::getenv("SLAT_NO_BATCH");
+    static const bool kNoBatch = std::getenv("SLAT_NO_BATCH") != nullptr;
+    const bool sym_batched = hash && ell && !kNoBatch;
     const bool batched = sym_batched && (dt != SLAT_F64 || f64any);
     if (sym_batched) {
         uint32_t cb = 1;
@@ -679,16 +707,19 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         const char *e = std::getenv("SLAT_SYM_BPC");
         return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 16ull;
     }();
+    // (the batched short-row tiles: twice the resident blocks, so blocks that drew cheap tiles
+    // make room for more: C4 numeric 1.00 -> 0.91 ms, profiles/r03_ab_dyn_xlane.txt)
     static const uint64_t kNumOver = [] {
         const char *e = std::getenv("SLAT_NUM_OVER");
-        return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 1ull;
+        return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 2ull;
     }();
     const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * kSymBpc)));
     const int sem = dt == SLAT_U32 ? kSemU32 : dt == SLAT_SAT64 ? kSemSat64 : f64any ? kSemF64Any : kSemF64;
     const int hash_mode = batched ? 3 : 1;  // numeric instance of the short rows of a wide launch
     auto num_grid = [&](int mode, size_t lds) {
         const int nbpc = slat_numeric_blocks_per_cu(sem, mode, idx32, ell, lds);
-        return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc * kNumOver)));
+        const uint64_t over = mode == 3 ? kNumOver : 1;
+        return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc * over)));
     };
     const dim3 grid = num_grid(hash ? 2 : 0, num_lds);
     const dim3 hash_grid = hash ? num_grid(hash_mode, hash_lds) : dim3(1);
@@ -703,13 +734,16 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const size_t eng_b = ell ? up256(B->n_rows) : 0;
     // stored bitmaps (single-window launches): symbolic keeps each row's touched bitmap blocks for
     // numeric, n * ww words at most (only touched blocks are written), capped against free memory
-    if (ctx->free_age++ % 32 == 0) {
+    // free device memory: re-read when this context's pool grew or shrank, else every 1024 calls
+    // (the query costs tens of microseconds of host time)
+    if (ctx->mem_changed || ctx->free_age++ % 1024 == 0) {
         size_t total_b = 0;
         (void)hipMemGetInfo(&ctx->free_b, &total_b);
+        ctx->mem_changed = false;
     }
     const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
-    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) &&
-                     !std::getenv("SLAT_NO_SBM");
+    static const bool kNoSbm = std::getenv("SLAT_NO_SBM") != nullptr;
+    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny;
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
@@ -720,7 +754,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // max row of A x max row of B (A's max row unknown: when B has long rows)
     static const bool kNoFat = std::getenv("SLAT_NO_FAT") != nullptr;
     const uint64_t maxrow_a = A->max_row_nnz;
-    const bool fat = !kNoFat && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
+    const bool fat = !kNoFat && !tiny && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
@@ -735,7 +769,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             a.b_vmax = ctx->d_vmax;
             a.epoch = ++ctx->epoch;
         }
-    } else if (dt != SLAT_F64 && kNarrowCsr) {
+    } else if (dt != SLAT_F64 && kNarrowCsr && !tiny) {
         // B walked in CSR form: k_bvmax gives the numeric pass the same max(B) (narrow slots, and
         // hub rows accumulate in C instead of one re-traversal per rank chunk)
         a.b_vmax = ctx->d_vmax;
@@ -808,112 +842,149 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     asym.sbm = a.sbm;
     asym.smask = a.smask;
     asym.nblk = a.nblk;
-    if (ell) {
-        hipError_t be;
-        if (dt == SLAT_U32)
-            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
-                                            (unsigned long long *)(ws + o_part));
-        else if (dt == SLAT_SAT64)
-            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
-                                                      (unsigned long long *)(ws + o_part));
-        else
-            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
-        SLAT_HIPC(be);
-    } else if (a.b_vmax && B->nnz) {
-        const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
-        if (dt == SLAT_U32)
-            hipLaunchKernelGGL(k_bvmax<uint32_t>, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz,
-                               ctx->d_vmax, a.epoch);
-        else
-            hipLaunchKernelGGL(k_bvmax<unsigned long long>, dim3(g), dim3(kBlock), 0, s,
-                               (const unsigned long long *)B->values, B->nnz, ctx->d_vmax, a.epoch);
-        SLAT_HIPC(hipGetLastError());
-    }
-    slat::FatArgs fat_args = {};
-    slat::FatArgs *fa = &fat_args;
-    if (fat) {
-        if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return failc(st);
-        asym.fr_mark = a.fr_mark;
-    }
-    if (ablate & 7u) {
-        // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded
-        Args abl = asym;
-        abl.ablate = ablate;
-        abl.counts = (uint64_t *)(ws + o_abl);
-        abl.c_rp = abl.counts;  // row_ptr[0] store lands in scratch too
-        SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
-        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, abl));
-        SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
-    }
-    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[0], s));
-    if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return failc(st);
-    if (sym_batched) {
-        // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
-        // row's products per tile, listing the rest), then the listed rows by windows
-        unsigned int *lc = (unsigned int *)(ws + o_lc);
-        SLAT_HIPC(hipMemsetAsync(lc, 0, lc_b, s));
-        Args h1 = asym, h2 = asym;
-        h1.cbits = a.cbits;
-        h1.list = h2.list = (uint32_t *)(ws + o_l1);
-        h1.list_cnt = h2.list_cnt = lc;
-        const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kWave - 1) / kWave / wpb + 1, ctx->cu_count * 16ull)));
-        SLAT_HIPC(slat_launch_symbolic_short(idx32, g1, wpb * sym_short_bytes(), s, h1));
-        SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
-        a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
-        a.list_cnt = lc + 16;
-    } else if (hash) {
-        SLAT_HIPC(slat_launch_symbolic(1, idx32, ell, sym_grid, sym_hash_lds, s, asym));
-        SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, asym));
-    } else {
-        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
-    }
-    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
-    // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
-    const bool bpart = ell && dt != SLAT_F64;
-    if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
-                               bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
-                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch)))
-        return failc(st);
-    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
-
-    if (exact) {
-        SLAT_HIPC(hipStreamSynchronize(s));
-        const uint64_t total = ctx->h_out[0];
-        C->capacity = std::max<uint64_t>(total, 1);
-        if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
-            slat_dev_alloc(ctx, &C->values, C->capacity * vs, s) != hipSuccess) {
-            slat_csr_free(ctx, C);
-            return fail(ctx, SLAT_EOOM, "C allocation failed");
-        }
-        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
-    }
-    a.c_col = C->col_idx;
-    a.c_val = C->values;
     hipError_t e;
-    const int win_mode = hash ? 2 : 0;  // numeric instance of the window rows
-    auto launch_num = [&](const Args &x) { return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x); };
-    if (ablate & ~7u) {
-        // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
-        // the real numeric pass below overwrites everything it wrote
-        Args abl = a;
-        abl.ablate = ablate;
-        abl.counts = (uint64_t *)(ws + o_abl);
-        SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
-        SLAT_HIPC(launch_num(abl));
-        SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
+    const bool run_tiny = tiny && !exact;
+    if (run_tiny) {
+        // the whole call in one cooperative kernel (slat_tiny.hip): at most one block per CU, a
+        // wave per row; its non-zero counts go to the second counts array
+        a.c_col = C->col_idx;
+        a.c_val = C->values;
+        a.seq = ++ctx->done_seq;
+        a.done = ctx->d_words + 6;
+        uint64_t *counts2 = (uint64_t *)(ws + o_abl);
+        const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(row_blocks, (uint64_t)ctx->cu_count));
+        const unsigned long long target = ctx->tiny_arrivals + g;
+        SLAT_HIPC(slat_launch_tiny(sem, dim3(g), num_lds, s, a, counts2, ctx->d_words + 7, target));
+        ctx->tiny_arrivals = target;
+        a.counts = counts2;
+    } else {
+        if (ell) {
+            hipError_t be;
+            if (dt == SLAT_U32)
+                be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
+                                                (unsigned long long *)(ws + o_part));
+            else if (dt == SLAT_SAT64)
+                be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
+                                                          (unsigned long long *)(ws + o_part));
+            else
+                be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
+            SLAT_HIPC(be);
+        } else if (a.b_vmax && B->nnz) {
+            const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
+            if (dt == SLAT_U32)
+                hipLaunchKernelGGL(k_bvmax<uint32_t>, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz,
+                                   ctx->d_vmax, a.epoch);
+            else
+                hipLaunchKernelGGL(k_bvmax<unsigned long long>, dim3(g), dim3(kBlock), 0, s,
+                                   (const unsigned long long *)B->values, B->nnz, ctx->d_vmax, a.epoch);
+            SLAT_HIPC(hipGetLastError());
+        }
+        slat::FatArgs fat_args = {};
+        slat::FatArgs *fa = &fat_args;
+        if (fat) {
+            if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return failc(st);
+            asym.fr_mark = a.fr_mark;
+        }
+        if (ablate & 7u) {
+            // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded
+            Args abl = asym;
+            abl.ablate = ablate;
+            abl.counts = (uint64_t *)(ws + o_abl);
+            abl.c_rp = abl.counts;  // row_ptr[0] store lands in scratch too
+            SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
+            SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, abl));
+            SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
+        }
+        // work distribution (SLAT_DYN bits, A/B knob; tickets in d_words[5]): 1 = the batched short-row
+        // tiles, 2 = the rows of the wide launches' window / one-row-hash passes (long, uneven rows:
+        // R-MAT 2^16 A^2 18.0 -> 14.3 ms), 4 = the single-window pass's rows (27k rows take a ticket
+        // each from one word: 30^3 A^6*A numeric 91 -> 383 us). Else a fixed stride over the grid.
+        static const uint32_t kDyn = [] {
+            const char *e = std::getenv("SLAT_DYN");
+            return e ? (uint32_t)std::atoi(e) : 2u;
+        }();
+        unsigned long long *tq = ctx->d_words + 5;
+        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[0], s));
+        if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return failc(st);
+        if (sym_batched) {
+            // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
+            // row's products per tile, listing the rest), then the listed rows by windows
+            unsigned int *lc = (unsigned int *)(ws + o_lc);
+            SLAT_HIPC(hipMemsetAsync(lc, 0, lc_b, s));
+            Args h1 = asym, h2 = asym;
+            h1.cbits = a.cbits;
+            h1.list = h2.list = (uint32_t *)(ws + o_l1);
+            h1.list_cnt = h2.list_cnt = lc;
+            const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kWave - 1) / kWave / wpb + 1, ctx->cu_count * 16ull)));
+            SLAT_HIPC(slat_launch_symbolic_short(idx32, g1, wpb * sym_short_bytes(), s, h1));
+            h2.tq = (kDyn & 2u) ? tq : nullptr;
+            SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
+            a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
+            a.list_cnt = lc + 16;
+        } else if (hash) {
+            Args h1 = asym;
+            h1.tq = (kDyn & 2u) ? tq : nullptr;
+            SLAT_HIPC(slat_launch_symbolic(1, idx32, ell, sym_grid, sym_hash_lds, s, h1));
+            SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h1));
+        } else {
+            SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
+        }
+        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
+        // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
+        const bool bpart = ell && dt != SLAT_F64;
+        if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
+                                   bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
+                                   bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch)))
+            return failc(st);
+        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
+
+        if (exact) {
+            SLAT_HIPC(hipStreamSynchronize(s));
+            const uint64_t total = ctx->h_out[0];
+            C->capacity = std::max<uint64_t>(total, 1);
+            if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
+                slat_dev_alloc(ctx, &C->values, C->capacity * vs, s) != hipSuccess) {
+                slat_csr_free(ctx, C);
+                return fail(ctx, SLAT_EOOM, "C allocation failed");
+            }
+            if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
+        }
+        a.c_col = C->col_idx;
+        a.c_val = C->values;
+        const int win_mode = hash ? 2 : 0;  // numeric instance of the window rows
+        auto launch_num = [&](const Args &x) { return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x); };
+        if (ablate & ~7u) {
+            // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
+            // the real numeric pass below overwrites everything it wrote
+            Args abl = a;
+            abl.ablate = ablate;
+            abl.counts = (uint64_t *)(ws + o_abl);
+            SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
+            SLAT_HIPC(launch_num(abl));
+            SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
+        }
+        if (hash) {
+            Args h1 = a;
+            if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
+            h1.tq = (kDyn & (hash_mode == 3 ? 1u : 2u)) ? tq : nullptr;
+            SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
+        }
+        a.tq = (kDyn & (hash ? 2u : 4u)) ? tq : nullptr;
+        // the window pass is the call's last kernel unless fat rows or the stats copy follow: it stores
+        // the completion word itself (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
+        static const bool kFusedSignal = std::getenv("SLAT_NO_FUSED_SIGNAL") == nullptr;
+        if (kFusedSignal && !fat && !a.stats && wait_mode() == 0) {
+            a.seq = ++ctx->done_seq;
+            a.done = ctx->d_words + 6;
+        }
+        SLAT_HIPC(launch_num(a));
+        if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return failc(st);
     }
-    if (hash) {
-        Args h1 = a;
-        if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
-        SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
-    }
-    SLAT_HIPC(launch_num(a));
-    if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return failc(st);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));
     if (a.stats) SLAT_HIPC(hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                              hipMemcpyDeviceToHost, s));
     hc.mark(1);
-    SLAT_HIPC(wait_stream(ctx, s));
+    SLAT_HIPC(wait_stream(ctx, s, a.seq));
 #undef SLAT_HIPC
     hc.mark(2);
     if (SLAT_PHASES) {
@@ -984,7 +1055,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     S.nnz = nnz;
     S.flops = flops;
     S.capacity = C->capacity;
-    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u);
+    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;

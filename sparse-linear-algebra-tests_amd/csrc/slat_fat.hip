@@ -110,7 +110,8 @@ __device__ __forceinline__ void b_range(const uint32_t *bcol, I bs, I be, uint32
 constexpr int kQ = 4;
 template <typename S, bool VALS, typename I, typename F>
 __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, uint32_t hi, bool all_cols, F &&fn,
-                                        const uint32_t *split = nullptr, uint32_t nch1 = 0, uint32_t chunk = 0) {
+                                        const uint32_t *split = nullptr, uint32_t nch1 = 0, uint32_t g0 = 0,
+                                        uint32_t g1 = 0) {
     const int lane = lane_id();
     const int wv = threadIdx.x / kWave;
     const S *av = (const S *)p.a_val;
@@ -133,9 +134,9 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
             if (k[Q] < p.b_nrows) {
                 if (split) {  // only the chunk's part of the B row: no filtering, no search
                     const I r = (I)p.b_rp[k[Q]];
-                    const uint32_t *sp = split + (uint64_t)k[Q] * nch1 + chunk;
-                    bs[Q] = r + (I)sp[0];
-                    be[Q] = r + (I)sp[1];
+                    const uint32_t *sp = split + (uint64_t)k[Q] * nch1;
+                    bs[Q] = r + (I)sp[g0];
+                    be[Q] = r + (I)sp[g1];
                 } else {
                     bs[Q] = (I)p.b_rp[k[Q]];
                     be[Q] = (I)p.b_rp[k[Q] + 1];
@@ -289,13 +290,73 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
     const Args &p = f.a;
     const S *av = (const S *)p.a_val;
     const S *bv = (const S *)p.b_val;
+    // the chunk's granules in the split table: [g0, g1)
+    const uint32_t g0 = c0 >> f.gsh, g1 = min(f.nch1 - 1, (c1 + (1u << f.gsh) - 1) >> f.gsh);
     if constexpr (!Sem::kOrdered) {
         const bool all = c0 == 0 && c1 == p.ncols;
         fr_walk<S, true, I>(p, a0, a1, c0, c1, all, [&](uint32_t c, S a, S b) {
             const uint32_t o = c - c0;
             Sem::acc(acc, o, Sem::prod(a, b));
             atomicOr(&bits[o >> 5], 1u << (o & 31));
-        }, f.split, f.nch1, c0 / fr_chunk<Sem>());
+        }, f.split, f.nch1, g0, g1);
+    } else if (f.split && (1u << f.gsh) * kFW == fr_chunk<Sem>()) {
+        // the split table's granule is one wave's slice: each A entry's part of the B row is two
+        // loads, no search. Entries with a non-empty part, in A order; the next one's B entries
+        // load while this one's products are added.
+        const int lane = lane_id(), wv = threadIdx.x / kWave;
+        const uint32_t g = g0 + (uint32_t)wv;
+        if ((c0 + ((uint32_t)wv << f.gsh)) >= c1) return;
+        for (I base = a0; base < a1; base += (I)kWave) {
+            const I i = base + (I)lane;
+            S a = S(0);
+            I bs = 0, be = 0;
+            if (i < a1) {
+                const uint32_t k = p.a_col[i];
+                a = av[i];
+                if (k < p.b_nrows) {
+                    const I r = (I)p.b_rp[k];
+                    const uint32_t *sp = f.split + (uint64_t)k * f.nch1 + g;
+                    bs = r + (I)sp[0];
+                    be = r + (I)sp[1];
+                }
+            }
+            unsigned long long m = __ballot(bs != be);
+            uint32_t cn = 0;
+            S vn = S(0), an = S(0);
+            I sn = 0, en = 0;
+            auto fetch = [&](int t) {
+                sn = (I)readlane_u64((uint64_t)bs, t);
+                en = (I)readlane_u64((uint64_t)be, t);
+                an = readlane_val(a, t);
+                if (sn + (I)lane < en) {
+                    cn = p.b_col[sn + (I)lane];
+                    vn = bv[sn + (I)lane];
+                }
+            };
+            if (m) fetch((int)__builtin_ctzll(m));
+            while (m) {
+                const uint32_t c = cn;
+                const S v = vn, at = an;
+                const I s = sn, e = en;
+                m &= m - 1;
+                if (m) fetch((int)__builtin_ctzll(m));
+                if (s + (I)lane < e) {
+                    const uint32_t o = c - c0;
+                    acc[o] = __dadd_rn(acc[o], __dmul_rn(at, v));
+                    atomicOr(&bits[o >> 5], 1u << (o & 31));
+                }
+                wave_sync();  // this entry's adds land before the next entry's (same columns)
+                for (I j0 = s + (I)kWave; j0 < e; j0 += (I)kWave) {  // a part longer than a wave
+                    const I j = j0 + (I)lane;
+                    if (j < e) {
+                        const uint32_t o = p.b_col[j] - c0;
+                        acc[o] = __dadd_rn(acc[o], __dmul_rn(at, bv[j]));
+                        atomicOr(&bits[o >> 5], 1u << (o & 31));
+                    }
+                    wave_sync();
+                }
+            }
+        }
     } else {
         const int lane = lane_id(), wv = threadIdx.x / kWave;
         const uint32_t span = (c1 - c0 + kFW - 1) / kFW;
@@ -312,9 +373,9 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                 if (k < p.b_nrows) {
                     const I r = (I)p.b_rp[k];
                     if (f.split) {  // the chunk's part of the B row
-                        const uint32_t *sp = f.split + (uint64_t)k * f.nch1 + c0 / fr_chunk<Sem>();
-                        bs = r + (I)sp[0];
-                        be = r + (I)sp[1];
+                        const uint32_t *sp = f.split + (uint64_t)k * f.nch1;
+                        bs = r + (I)sp[g0];
+                        be = r + (I)sp[g1];
                     } else {
                         bs = r;
                         be = (I)p.b_rp[k + 1];
@@ -429,6 +490,7 @@ slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
     f.csh = csh;
     f.split = nullptr;
     f.nch1 = 0;
+    f.gsh = 0;
     SLAT_HIP(ctx, hipMemsetAsync(f.cnt, 0, 4, s));
     a.fr_mark = f.mark;
     f.a = a;
@@ -472,14 +534,24 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
     if ((1ull << h.csh) < fr_chunk<Sem>()) return hipErrorInvalidValue;
     // B split by this instance's accumulator chunk, so each chunk's walk loads only its own entries
     // (MAGNUS's column-chunk reordering, applied to B once instead of to every fat row's products)
-    const uint64_t nch = (h.a.ncols + fr_chunk<Sem>() - 1) / fr_chunk<Sem>();
+    // (f64 in the reference's order: granules of one wave's slice of a chunk when that table fits,
+    // so no wave searches its slice in a B row)
     const uint64_t nb = h.a.b_nrows;
+    uint32_t sh = (uint32_t)__builtin_ctz(fr_chunk<Sem>());
+    static const bool kNoSlices = std::getenv("SLAT_NO_FAT_SLICES") != nullptr;  // A/B knob
+    if (Sem::kOrdered && !kNoSlices) {
+        const uint32_t fine = sh - (uint32_t)__builtin_ctz((uint32_t)kFW);
+        const uint64_t ng = (h.a.ncols + (1ull << fine) - 1) >> fine;
+        if (nb * (ng + 1) * 4 <= kSplitBytes) sh = fine;
+    }
+    const uint64_t nch = (h.a.ncols + (1ull << sh) - 1) >> sh;  // granules
     uint32_t *split = nullptr;
     h.split = nullptr;
     h.nch1 = 0;
-    if (nch > 1 && nb * (nch + 1) * 4 <= kSplitBytes && !std::getenv("SLAT_NO_FAT_SPLIT")) {
+    h.gsh = sh;
+    static const bool kNoSplit = std::getenv("SLAT_NO_FAT_SPLIT") != nullptr;  // A/B knob
+    if (nch > 1 && nb * (nch + 1) * 4 <= kSplitBytes && !kNoSplit) {
         if (slat_dev_alloc(ctx, (void **)&split, nb * (nch + 1) * 4, ctx->stream) == hipSuccess) {
-            const uint32_t sh = (uint32_t)__builtin_ctz(fr_chunk<Sem>());
             const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb * (nch + 1) + kBlock - 1) / kBlock,
                                                                                    (uint64_t)ctx->cu_count * 16));
             hipLaunchKernelGGL(k_fr_splits, dim3(gs), dim3(kBlock), 0, ctx->stream, h.a.b_rp, h.a.b_col, nb,

@@ -14,10 +14,12 @@ struct FatArgs {
     uint8_t *mark;              // [n] 1 = fat
     unsigned long long *cmask;  // [list position] touched accumulator chunks (bit c: chunk c; 64 max)
     uint32_t csh;               // log2 of the chunk mask's granule (columns per mask bit)
-    // B split by accumulator chunk (numeric pass; null = none): split[k * nch1 + c] = the offset in B
-    // row k of its first entry with column >= c * chunk width (c = 0 .. nch1 - 1, the last = len)
+    // B split by column granule (numeric pass; null = none): split[k * nch1 + g] = the offset in B
+    // row k of its first entry with column >= g << gsh (g = 0 .. nch1 - 1, the last = len). The
+    // granule is the accumulator chunk, or for f64 in the reference's order one wave's slice of it
     const uint32_t *split;
     uint32_t nch1;
+    uint32_t gsh;
 };
 }  // namespace slat
 

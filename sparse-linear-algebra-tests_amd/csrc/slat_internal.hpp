@@ -26,7 +26,11 @@ struct slat_ctx {
     unsigned long long *h_out_dev = nullptr; // its device alias (written by k_scan_rows / k_numeric); [7]: the
                                              // end-of-call sequence word (k_signal)
     unsigned long long done_seq = 0;         // last sequence number queued to [7]
-    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word
+    unsigned long long tiny_arrivals = 0;    // k_tiny's grid-barrier arrivals so far (d_words[7], never reset)
+    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word,
+                                             // [4] check flags, [5] work tickets (zeroed by each launch's last taker),
+                                             // [6] blocks done of the call's last kernel (zeroed by its last block),
+                                             // [7] k_tiny's barrier arrivals (monotonic)
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
     unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
@@ -35,6 +39,7 @@ struct slat_ctx {
     uint32_t scan_epoch = 0;                 // tag of the status / max-row words (22 bits)
     size_t free_b = 0;                       // cached hipMemGetInfo free bytes
     uint32_t free_age = 0;
+    bool mem_changed = true;                 // the pool took or returned a chunk since free_b was read
     hipEvent_t ev[6] = {};
     // device memory: hipMalloc'd chunks carved into pieces. A freed piece is cached and handed out
     // again in stream order (slat_dev_alloc); adjacent free pieces of a chunk merge; a chunk goes

@@ -51,6 +51,9 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_PHASES
 #define SLAT_PHASES 0  // diagnostic builds: per-phase s_memtime cycles of k_numeric
 #endif
+#ifndef SLAT_AEARLY
+#define SLAT_AEARLY 1  // k_numeric: a long row's A values for the narrow bound loaded with its stored bitmap
+#endif
 #ifndef SLAT_SAT64_NARROW
 #define SLAT_SAT64_NARROW 1  // Sat64 rows under the u32 bound accumulate in u32 slots (variant builds: 0)
 #endif
@@ -112,9 +115,31 @@ struct Args {
     // rows of the fat-row category (slat_fat.hip: a workgroup and a dense LDS accumulator per row),
     // which the kernels here skip; null = none
     const uint8_t *fr_mark;
+    // rows (k_symbolic, k_numeric) or row tiles (k_numeric_short) from a ticket counter instead of
+    // a fixed stride over the grid (null)
+    unsigned long long *tq;
+    // the call's completion (seq != 0: this launch is the call's last kernel; signal_done)
+    unsigned long long *done;
+    unsigned long long seq;
 };
 
 __device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.fr_mark && p.fr_mark[row]; }
+
+// End of the call's last kernel (p.seq != 0): the last block to finish stores seq into the mapped host
+// word the host spins on (host_out[7]), in place of a one-thread kernel queued behind this one (a
+// dispatch of its own, ~4 us per call). Stream order still covers everything after the call; the
+// host learns of the end a few hundred ns before the grid has retired.
+__device__ __forceinline__ void signal_done(const Args &p) {
+    if (p.seq == 0) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long old = __hip_atomic_fetch_add(p.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == gridDim.x - 1) {
+            __hip_atomic_store(p.done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&p.host_out[7], p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
 
 // ------------------------------------------------------------------------------------------------
 // value semirings: S storage type, P cached product, V LDS accumulator
@@ -261,6 +286,69 @@ __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     return ((uint64_t)readlane_u32((uint32_t)(v >> 32), l) << 32) | readlane_u32((uint32_t)v, l);
 }
+
+// Work items handed out by a ticket counter instead of a fixed stride, so waves that drew cheap items
+// take more of them. Wave w starts on item w without a ticket (a wave with no item never touches
+// the counter: one contended address costs ~11 ns per atomic, so 16k waves taking one failing
+// ticket each would add ~180 us); after that, ticket t is item waves + t. One device-scope atomic per
+// later item, issued one item ahead (its latency overlaps the current item's loads). Every wave
+// that had an item takes exactly one ticket past the end, so the last taker knows it is last and
+// zeroes the counter for the next launch on the stream.
+struct TicketQueue {
+    unsigned long long *ctr;
+    uint64_t n, waves, total;  // items, waves in the grid, tickets this launch takes
+    __device__ __forceinline__ TicketQueue(unsigned long long *c, uint64_t items, uint64_t nw)
+        : ctr(c), n(items), waves(nw), total((items > nw ? items - nw : 0) + (items < nw ? items : nw)) {}
+    __device__ __forceinline__ unsigned long long issue() const {
+        unsigned long long t = 0;
+        if (lane_id() == 0) t = atomicAdd(ctr, 1ull);
+        return t;
+    }
+    // the item of a ticket (>= n: none left)
+    __device__ __forceinline__ uint64_t resolve(unsigned long long t) const {
+        const uint64_t v = readlane_u64(t, 0);
+        if (v == total - 1 && lane_id() == 0) __hip_atomic_store(ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return waves + v;
+    }
+};
+// Rows that lost explicit zeros (rare), counted straight into the mapped host word. In a launch that
+// signals the call's end the add returns its old value, so it has completed before the wave reaches
+// signal_done's barrier (the completion word must not overtake it).
+__device__ __forceinline__ void add_zero_rows(unsigned long long *word, uint32_t zrows, bool signals) {
+    if (lane_id() != 0 || zrows == 0) return;
+    if (signals) {
+        const unsigned long long old =
+            __hip_atomic_fetch_add(word, (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("" ::"v"(old));  // wait for the value
+    } else {
+        __hip_atomic_fetch_add(word, (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Static tile order with each XCD on a contiguous eighth of the tiles: workgroups go to the 8 XCDs
+// round-robin by blockIdx and every XCD has its own L2, so a plain stride over the grid spreads
+// neighbouring tiles (rows that gather neighbouring B rows) over all eight L2s. Here XCD x's waves
+// stride over [x * per, (x + 1) * per). SLAT_XCD=0: the plain stride.
+#ifndef SLAT_XCD
+#define SLAT_XCD 1
+#endif
+constexpr uint32_t kXcds = 8;
+struct XcdStride {
+    uint64_t first, end, stride;
+    __device__ __forceinline__ XcdStride(uint64_t n, int wpb, int wv) {
+        if (SLAT_XCD && gridDim.x >= 4 * kXcds) {
+            const uint32_t x = blockIdx.x % kXcds, nb = (gridDim.x - x + kXcds - 1) / kXcds;  // blocks on XCD x
+            const uint64_t per = (n + kXcds - 1) / kXcds;
+            first = x * per + (uint64_t)(blockIdx.x / kXcds) * wpb + wv;
+            end = min<uint64_t>(n, (x + 1) * per);
+            stride = (uint64_t)nb * wpb;
+        } else {
+            first = (uint64_t)blockIdx.x * wpb + wv;
+            end = n;
+            stride = (uint64_t)gridDim.x * wpb;
+        }
+    }
+};
 template <typename S>
 __device__ __forceinline__ S readlane_val(S v, int l) {
     if constexpr (sizeof(S) == 4) {
@@ -1326,7 +1414,11 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
-    for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it += stride) {
+    const bool dyn = p.tq != nullptr;  // launch-uniform
+    const TicketQueue tq(p.tq, nit, stride);
+    unsigned long long pend = 0;
+    for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
+        if (dyn) pend = tq.issue();
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
         if (fat_row(p, row)) continue;  // the fat-row kernels' row
         const uint64_t cnt = sym_row<I, ELL, MODE>(p, row, listed, L0, flops);
@@ -1410,7 +1502,11 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     using RW = RowWalker<Sem, I, ELL, kVals>;
-    for (uint64_t it = first; it < nit; it += stride) {
+    const bool dyn = p.tq != nullptr;  // launch-uniform
+    const TicketQueue tq(p.tq, nit, stride);
+    unsigned long long pend = 0;
+    for (uint64_t it = first; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
+        if (dyn) pend = tq.issue();
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
         if (fat_row(p, row)) continue;  // the fat-row kernels' row
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
@@ -1505,6 +1601,19 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
                 constexpr bool Z = decltype(ztag)::value;
                 const bool stored = Z && p.sbm != nullptr;  // launch-uniform
                 uint32_t bmask, wcnt = 0;
+                // a multi-segment row's first 512 A values for the narrow bound below, loaded
+                // ahead of its stored bitmap so both loads wait out one memory latency together
+                // (nothing has walked the row's later segments yet)
+                const bool aearly = SLAT_AEARLY && Sem::kNarrowable && stored && !rw.single && bvmax != 0xFFFFFFFFu;
+                S aq8[8];
+                if constexpr (Sem::kNarrowable)
+                    if (aearly) {
+                        const S *av = (const S *)p.a_val;
+                        sfor<8>([&](auto I_) {
+                            const I j = a0 + (I)lane + (I)(I_ * kWave);
+                            aq8[I_] = j < a1 ? av[j] : S(0);
+                        });
+                    }
                 if (stored) {
                     // 1'. the row's bitmap as symbolic left it: touched blocks only, loaded 8 blocks
                     //     at a time, ranked from registers and written whole ({bits, rank} per word),
@@ -1559,14 +1668,19 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
                 // max(A row) * max(B) * len(A row) < 2^32 (each output sums <= len products)
                 bool narrow = false;
                 if constexpr (Sem::kNarrowable) {
-                    // (rw.amax covers a one-segment row; a longer row reads its A values once more
-                    // here: with a stored bitmap nothing walked its later segments yet, so its
-                    // amax would hold nothing)
+                    // (rw.amax covers a one-segment row; a longer row reads its A values once more:
+                    // with a stored bitmap nothing walked its later segments yet, so its amax would
+                    // hold nothing)
                     if (bvmax != 0xFFFFFFFFu) {
                         uint32_t am = rw.amax;
                         if (!rw.single) {
+                            I j0 = a0;
+                            if (aearly) {
+                                sfor<8>([&](auto I_) { am = max(am, sat32(aq8[I_])); });
+                                j0 += (I)(8 * kWave);
+                            }
                             const S *av = (const S *)p.a_val;
-                            for (I j = a0 + (I)lane; j < a1; j += (I)kWave) am = max(am, sat32(av[j]));
+                            for (I j = j0 + (I)lane; j < a1; j += (I)kWave) am = max(am, sat32(av[j]));
                         }
                         const uint64_t x = (uint64_t)wave_max_u32(am) * bvmax;
                         narrow = x == 0 || len <= 0xFFFFFFFFull / x;
@@ -1710,9 +1824,7 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
             for (int i = 0; i < kPhaseSlots; ++i) atomicAdd(&dst[i], (unsigned long long)ph[i]);
         }
     }
-    // rows that lost explicit zeros (rare): counted straight into the mapped host word
-    if (lane == 0 && zrows)
-        __hip_atomic_fetch_add(&p.host_out[2], (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    add_zero_rows(&p.host_out[2], zrows, p.seq != 0);
 }
 
 template <typename Sem, typename I, bool ELL, int MODE = 0>
@@ -1721,6 +1833,7 @@ __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     constexpr int kWpb = kBlock / kWave;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
     numeric_rows<Sem, I, ELL, MODE>(p, smem8, wv, (uint64_t)blockIdx.x * kWpb + wv, (uint64_t)gridDim.x * kWpb);
+    signal_done(p);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1849,7 +1962,8 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
     const uint32_t cb = p.cbits;
     unsigned long long flops = 0;
     const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
-    for (uint64_t tile = (uint64_t)blockIdx.x * kWpb + wv; tile < ntiles; tile += (uint64_t)gridDim.x * kWpb) {
+    const XcdStride xs(ntiles, kWpb, wv);
+    for (uint64_t tile = xs.first; tile < xs.end; tile += xs.stride) {
         const uint64_t r0 = tile * kWave, r = r0 + lane;
         const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
         uint64_t A0j = 0, A1j = 0;
@@ -1949,7 +2063,9 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
 // emit order of the hash categories' keys.
 // ------------------------------------------------------------------------------------------------
 // value of lane (lane ^ M): DPP quad permutes for 1 and 2 (bound_ctrl: no old value to set up, every
-// lane reads a valid source), ds_swizzle (bit-mask mode, within 32 lanes) up to 16, ds_bpermute for 32
+// lane reads a valid source), ds_swizzle (bit-mask mode, within 32 lanes) up to 16, ds_bpermute for
+// 32. (DPP row_ror / half-mirror pairs for 4 and 8 and gfx950's permlane16/32 swaps for 16 and 32
+// measured no faster on C4's sorts: profiles/r03_ab_dyn_xlane.txt.)
 template <int M>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
     if constexpr (M == 1)
@@ -2146,7 +2262,14 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
     const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
     PhaseClock pc{};  // diagnostic builds (SLAT_PHASES): where the waves' time goes
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
-    for (uint64_t tile = (uint64_t)blockIdx.x * kWpb + wv; tile < ntiles; tile += (uint64_t)gridDim.x * kWpb) {
+    const bool dyn = p.tq != nullptr;  // launch-uniform
+    const TicketQueue tq(p.tq, ntiles, (uint64_t)gridDim.x * kWpb);
+    const XcdStride xs(ntiles, kWpb, wv);
+    unsigned long long pend = 0;
+    const uint64_t tend = dyn ? ntiles : xs.end;
+    for (uint64_t tile = dyn ? (uint64_t)blockIdx.x * kWpb + wv : xs.first; tile < tend;
+         tile = dyn ? tq.resolve(pend) : tile + xs.stride) {
+        if (dyn) pend = tq.issue();
         const uint64_t r0 = tile * kWave, r = r0 + lane;
         const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
         uint64_t A0j = 0, A1j = 0, obj = 0, oej = 0;
@@ -2277,14 +2400,13 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
             for (int i = 0; i < kPhaseSlots; ++i) atomicAdd(&dst[i], (unsigned long long)pc.ph[i]);
         }
     }
-    zrows = wave_sum_u32(zrows);
-    if (lane == 0 && zrows)
-        __hip_atomic_fetch_add(&p.host_out[2], (unsigned long long)zrows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    add_zero_rows(&p.host_out[2], wave_sum_u32(zrows), p.seq != 0);
 }
 
 template <typename Sem0, typename I>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_numeric_short(Args p) {
     numeric_short_body<Sem0, I>(p);
+    signal_done(p);
 }
 // u32: 5 waves per SIMD (6.6 KB of LDS per wave, <= 96 VGPRs; the wider semirings are held to 4
 // waves by their LDS anyway). At 6 waves (<= 80 VGPRs) 28 VGPRs spilled to scratch and C4's numeric
@@ -2300,6 +2422,7 @@ __attribute__((amdgpu_waves_per_eu(SLAT_SHORT_WPE)))
 #endif
 void k_numeric_short_u32(Args p) {
     numeric_short_body<SemU32, I>(p);
+    signal_done(p);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2373,11 +2496,7 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
     __shared__ uint32_t wmax[kScanThreads / kWave];
     const int t = threadIdx.x, lane = lane_id(), w = t / kWave;
     const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
-    const unsigned long long tag = (unsigned long long)epoch << 42;
     auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto st = [](unsigned long long *x, unsigned long long v) {
-        __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
     if (t == 0) s_bcast[0] = atomicAdd(ticket, 1ull) - ticket_base;
     __syncthreads();
     const uint64_t tile = s_bcast[0];

@@ -3,8 +3,9 @@
 window categories): RG = R-MAT 2^16 undirected u32 A^2, C5 = R-MAT 2^16 (and --big: 2^18) degree 16
 f64 A*A in any order and in the reference's fold order, chain = directed R-MAT 2^14 A^4 * A.
 
-usage: python tools/ab_heavy.py [--reps R] [--big] VARIANT...  (VARIANT as in tools/ab.py:
-"tree", NAME for tools/var/libslat_NAME.so, NAME:ENV=VAL,... for env knobs)
+usage: python tools/ab_heavy.py [--reps R] [--big] [--legs rg,c5any,...] VARIANT...  (VARIANT as in
+tools/ab.py: "tree", NAME for tools/var/libslat_NAME.so, NAME:ENV=VAL,... for env knobs);
+python tools/ab_heavy.py --child [--big] [--legs ...] runs the legs once in this process (profiling)
 
 Children alternate in order; each prints the best-of-2 ms per leg (after one warm-up call), its
 symbolic / numeric event split, and the output nnz against the known count.
@@ -21,7 +22,7 @@ NNZ = {"rg": 164123598, "c5any": 163990080, "c5ord": 163990080, "chain": 8429521
        "c5big_any": 1277823132, "c5big_ord": 1277823132}
 
 
-def child(big: bool):
+def child(big: bool, legs=None):
     sys.path.insert(0, os.path.join(ROOT, "sparse-linear-algebra-tests_amd"))
     import numpy as np
 
@@ -30,6 +31,8 @@ def child(big: bool):
     out = {}
 
     def run(name, a, b, flags=0, reps=2):
+        if legs and name not in legs:
+            return
         best, st, nz = 1e30, None, 0
         c = a._spgemm(b, flags)
         del c
@@ -45,22 +48,26 @@ def child(big: bool):
         out[name] = {"ms": round(best, 3), "sym": round(st["symbolic_ms"], 3), "num": round(st["numeric_ms"], 3),
                      "ok": nz == NNZ[name]}
 
-    h = slat.host_rmat(16, (1 << 16) * 8)
-    rows = np.repeat(np.arange(h.n, dtype=np.uint32), np.diff(h.row_ptr).astype(np.int64))
-    a = slat.CsrMatrix.from_edges_device(h.n, rows, h.col_idx, True, ctx)
-    run("rg", a, a)
-    del a
-    f = slat.CsrF64.from_host(slat.host_rmat(16, (1 << 16) * 16), ctx)
-    run("c5any", f, f, slat.FLAG_F64_ANY_ORDER)
-    run("c5ord", f, f, 0, 1)
-    del f
-    h = slat.host_rmat(14, (1 << 14) * 8)
-    rows = np.repeat(np.arange(h.n, dtype=np.uint32), np.diff(h.row_ptr).astype(np.int64))
-    d = slat.CsrMatrix.from_edges_device(h.n, rows, h.col_idx, False, ctx)
-    p = d.matmul(d).matmul(d).matmul(d)
-    run("chain", p, d)
-    del p, d
-    if big:
+    want = lambda *ns: not legs or any(n in legs for n in ns)  # noqa: E731
+    if want("rg"):
+        h = slat.host_rmat(16, (1 << 16) * 8)
+        rows = np.repeat(np.arange(h.n, dtype=np.uint32), np.diff(h.row_ptr).astype(np.int64))
+        a = slat.CsrMatrix.from_edges_device(h.n, rows, h.col_idx, True, ctx)
+        run("rg", a, a)
+        del a
+    if want("c5any", "c5ord"):
+        f = slat.CsrF64.from_host(slat.host_rmat(16, (1 << 16) * 16), ctx)
+        run("c5any", f, f, slat.FLAG_F64_ANY_ORDER)
+        run("c5ord", f, f, 0, 1)
+        del f
+    if want("chain"):
+        h = slat.host_rmat(14, (1 << 14) * 8)
+        rows = np.repeat(np.arange(h.n, dtype=np.uint32), np.diff(h.row_ptr).astype(np.int64))
+        d = slat.CsrMatrix.from_edges_device(h.n, rows, h.col_idx, False, ctx)
+        p = d.matmul(d).matmul(d).matmul(d)
+        run("chain", p, d)
+        del p, d
+    if big and want("c5big_any", "c5big_ord"):
         f = slat.CsrF64.from_host(slat.host_rmat(18, (1 << 18) * 16), ctx)
         run("c5big_any", f, f, slat.FLAG_F64_ANY_ORDER, 1)
         run("c5big_ord", f, f, 0, 1)
@@ -72,10 +79,12 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--big", action="store_true")
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--legs", default="", help="comma-separated subset of the legs")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
+    legs = [x for x in a.legs.split(",") if x]
     if a.child:
-        child(a.big)
+        child(a.big, legs)
         return
     res = {}
     for r in range(a.reps):
@@ -88,7 +97,8 @@ def main():
             for kv in filter(None, knobs.split(",")):
                 k, _, val = kv.partition("=")
                 env[k] = val
-            cmd = [sys.executable, os.path.abspath(__file__), "--child"] + (["--big"] if a.big else [])
+            cmd = ([sys.executable, os.path.abspath(__file__), "--child"] + (["--big"] if a.big else [])
+                   + (["--legs", a.legs] if legs else []))
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
             if p.returncode != 0:
                 print(f"{v}: FAILED rc={p.returncode}\n{p.stderr[-3000:]}", flush=True)
