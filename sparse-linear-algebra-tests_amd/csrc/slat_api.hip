@@ -441,11 +441,12 @@ slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, 
         SLAT_HIP(ctx, hipMemsetAsync(ctx->d_words + 2, 0, 8, s));
         ctx->scan_epoch = 1;
     }
+    const bool ticketed = tiles > (uint64_t)ctx->cu_count;
     hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status,
-                       ctx->d_words + 1, ctx->ticket_base, ctx->scan_epoch, ctx->d_words + 2, ctx->h_out_dev, bpart,
-                       nbpart, ctx->d_vmax, vepoch);
+                       ticketed ? ctx->d_words + 1 : nullptr, ctx->ticket_base, ctx->scan_epoch, ctx->d_words + 2,
+                       ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch);
     SLAT_HIP(ctx, hipGetLastError());
-    ctx->ticket_base += tiles;
+    if (ticketed) ctx->ticket_base += tiles;
     return SLAT_OK;
 }
 
@@ -660,18 +661,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // padded ELL copy of B when its rows are short (bounded blow-up)
     const uint64_t wq = (maxrow_b + 3) / 4;
     const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
-    // small products: the whole call in one kernel (slat_tiny.hip) — one window of at most 8192
-    // columns, 32-bit offsets, a product bound that a wave per row finishes in microseconds, and no
-    // per-pass timing or stats (those report the regular pipeline's passes)
-    static const bool kNoTiny = std::getenv("SLAT_NO_TINY") != nullptr;
-    const bool tiny = !kNoTiny && !asym.wide && ncols <= 8192 && n <= 4096 && idx32 && wait_mode() == 0 &&
-                      !(flags & (SLAT_FLAG_TIMING | SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) &&
-                      g_progress.load(std::memory_order_relaxed) == 0 &&
-                      (unsigned __int128)a_nnz_block * maxrow_b <= (1u << 18);
     static const bool kNoEll = std::getenv("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
-                     !kNoEll && !tiny;  // 24-bit row index, 31-bit byte offsets in the kernels
+                     !kNoEll;  // 24-bit row index, 31-bit byte offsets in the kernels
 
     // LDS sizing and grids. The numeric grid is the kernel's resident capacity (waves stride over
     // rows; measured faster than oversubscribing); symbolic takes up to 16 blocks per CU.
@@ -743,7 +736,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
     static const bool kNoSbm = std::getenv("SLAT_NO_SBM") != nullptr;
-    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny;
+    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm;
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
@@ -754,7 +747,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // max row of A x max row of B (A's max row unknown: when B has long rows)
     static const bool kNoFat = std::getenv("SLAT_NO_FAT") != nullptr;
     const uint64_t maxrow_a = A->max_row_nnz;
-    const bool fat = !kNoFat && !tiny && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
+    const bool fat = !kNoFat && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
@@ -769,7 +762,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             a.b_vmax = ctx->d_vmax;
             a.epoch = ++ctx->epoch;
         }
-    } else if (dt != SLAT_F64 && kNarrowCsr && !tiny) {
+    } else if (dt != SLAT_F64 && kNarrowCsr) {
         // B walked in CSR form: k_bvmax gives the numeric pass the same max(B) (narrow slots, and
         // hub rows accumulate in C instead of one re-traversal per rank chunk)
         a.b_vmax = ctx->d_vmax;
@@ -784,6 +777,29 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     a.host_out = ctx->h_out_dev;
     ctx->h_out[0] = ctx->h_out[1] = ctx->h_out[2] = 0;  // no kernel of this context is in flight
+    // the ELL image (or B's value summary) first: it runs while the host allocates C and queues
+    // the rest, instead of after the host's setup with the GPU idle
+    if (ell) {
+        hipError_t be;
+        if (dt == SLAT_U32)
+            be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
+                                            (unsigned long long *)(ws + o_part));
+        else if (dt == SLAT_SAT64)
+            be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
+                                                      (unsigned long long *)(ws + o_part));
+        else
+            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
+        SLAT_HIP(ctx, be);
+    } else if (a.b_vmax && B->nnz) {
+        const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
+        if (dt == SLAT_U32)
+            hipLaunchKernelGGL(k_bvmax<uint32_t>, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz,
+                               ctx->d_vmax, a.epoch);
+        else
+            hipLaunchKernelGGL(k_bvmax<unsigned long long>, dim3(g), dim3(kBlock), 0, s,
+                               (const unsigned long long *)B->values, B->nnz, ctx->d_vmax, a.epoch);
+        SLAT_HIP(ctx, hipGetLastError());
+    }
 
     // capacity by exact bound (no mid-call sync) unless it exceeds the budget
     unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
@@ -843,143 +859,106 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     asym.smask = a.smask;
     asym.nblk = a.nblk;
     hipError_t e;
-    const bool run_tiny = tiny && !exact;
-    if (run_tiny) {
-        // the whole call in one cooperative kernel (slat_tiny.hip): at most one block per CU, a
-        // wave per row; its non-zero counts go to the second counts array
-        a.c_col = C->col_idx;
-        a.c_val = C->values;
+    slat::FatArgs fat_args = {};
+    slat::FatArgs *fa = &fat_args;
+    if (fat) {
+        if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return failc(st);
+        asym.fr_mark = a.fr_mark;
+    }
+    if (ablate & 7u) {
+        // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded
+        Args abl = asym;
+        abl.ablate = ablate;
+        abl.counts = (uint64_t *)(ws + o_abl);
+        abl.c_rp = abl.counts;  // row_ptr[0] store lands in scratch too
+        SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
+        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, abl));
+        SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
+    }
+    // work distribution (SLAT_DYN bits, A/B knob; tickets in d_words[5]): 1 = the batched short-row
+    // tiles, 2 = the rows of the wide launches' window / one-row-hash passes (long, uneven rows:
+    // R-MAT 2^16 A^2 18.0 -> 14.3 ms), 4 = the single-window pass's rows (27k rows take a ticket
+    // each from one word: 30^3 A^6*A numeric 91 -> 383 us). Else a fixed stride over the grid.
+    static const uint32_t kDyn = [] {
+        const char *e = std::getenv("SLAT_DYN");
+        return e ? (uint32_t)std::atoi(e) : 2u;
+    }();
+    unsigned long long *tq = ctx->d_words + 5;
+    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[0], s));
+    if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return failc(st);
+    if (sym_batched) {
+        // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
+        // row's products per tile, listing the rest), then the listed rows by windows
+        unsigned int *lc = (unsigned int *)(ws + o_lc);
+        SLAT_HIPC(hipMemsetAsync(lc, 0, lc_b, s));
+        Args h1 = asym, h2 = asym;
+        h1.cbits = a.cbits;
+        h1.list = h2.list = (uint32_t *)(ws + o_l1);
+        h1.list_cnt = h2.list_cnt = lc;
+        const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kWave - 1) / kWave / wpb + 1, ctx->cu_count * 16ull)));
+        SLAT_HIPC(slat_launch_symbolic_short(idx32, g1, wpb * sym_short_bytes(), s, h1));
+        h2.tq = (kDyn & 2u) ? tq : nullptr;
+        SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
+        a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
+        a.list_cnt = lc + 16;
+    } else if (hash) {
+        Args h1 = asym;
+        h1.tq = (kDyn & 2u) ? tq : nullptr;
+        SLAT_HIPC(slat_launch_symbolic(1, idx32, ell, sym_grid, sym_hash_lds, s, h1));
+        SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h1));
+    } else {
+        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
+    }
+    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
+    // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
+    const bool bpart = ell && dt != SLAT_F64;
+    if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
+                               bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
+                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch)))
+        return failc(st);
+    if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
+
+    if (exact) {
+        SLAT_HIPC(hipStreamSynchronize(s));
+        const uint64_t total = ctx->h_out[0];
+        C->capacity = std::max<uint64_t>(total, 1);
+        if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
+            slat_dev_alloc(ctx, &C->values, C->capacity * vs, s) != hipSuccess) {
+            slat_csr_free(ctx, C);
+            return fail(ctx, SLAT_EOOM, "C allocation failed");
+        }
+        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
+    }
+    a.c_col = C->col_idx;
+    a.c_val = C->values;
+    const int win_mode = hash ? 2 : 0;  // numeric instance of the window rows
+    auto launch_num = [&](const Args &x) { return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x); };
+    if (ablate & ~7u) {
+        // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
+        // the real numeric pass below overwrites everything it wrote
+        Args abl = a;
+        abl.ablate = ablate;
+        abl.counts = (uint64_t *)(ws + o_abl);
+        SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
+        SLAT_HIPC(launch_num(abl));
+        SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
+    }
+    if (hash) {
+        Args h1 = a;
+        if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
+        h1.tq = (kDyn & (hash_mode == 3 ? 1u : 2u)) ? tq : nullptr;
+        SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
+    }
+    a.tq = (kDyn & (hash ? 2u : 4u)) ? tq : nullptr;
+    // the window pass is the call's last kernel unless fat rows or the stats copy follow: it stores
+    // the completion word itself (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
+    static const bool kFusedSignal = std::getenv("SLAT_NO_FUSED_SIGNAL") == nullptr;
+    if (kFusedSignal && !fat && !a.stats && wait_mode() == 0) {
         a.seq = ++ctx->done_seq;
         a.done = ctx->d_words + 6;
-        uint64_t *counts2 = (uint64_t *)(ws + o_abl);
-        const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(row_blocks, (uint64_t)ctx->cu_count));
-        const unsigned long long target = ctx->tiny_arrivals + g;
-        SLAT_HIPC(slat_launch_tiny(sem, dim3(g), num_lds, s, a, counts2, ctx->d_words + 7, target));
-        ctx->tiny_arrivals = target;
-        a.counts = counts2;
-    } else {
-        if (ell) {
-            hipError_t be;
-            if (dt == SLAT_U32)
-                be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
-                                                (unsigned long long *)(ws + o_part));
-            else if (dt == SLAT_SAT64)
-                be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
-                                                          (unsigned long long *)(ws + o_part));
-            else
-                be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
-            SLAT_HIPC(be);
-        } else if (a.b_vmax && B->nnz) {
-            const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
-            if (dt == SLAT_U32)
-                hipLaunchKernelGGL(k_bvmax<uint32_t>, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz,
-                                   ctx->d_vmax, a.epoch);
-            else
-                hipLaunchKernelGGL(k_bvmax<unsigned long long>, dim3(g), dim3(kBlock), 0, s,
-                                   (const unsigned long long *)B->values, B->nnz, ctx->d_vmax, a.epoch);
-            SLAT_HIPC(hipGetLastError());
-        }
-        slat::FatArgs fat_args = {};
-        slat::FatArgs *fa = &fat_args;
-        if (fat) {
-            if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return failc(st);
-            asym.fr_mark = a.fr_mark;
-        }
-        if (ablate & 7u) {
-            // experiments only: an ablated symbolic pass into scratch counts, timed, then discarded
-            Args abl = asym;
-            abl.ablate = ablate;
-            abl.counts = (uint64_t *)(ws + o_abl);
-            abl.c_rp = abl.counts;  // row_ptr[0] store lands in scratch too
-            SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
-            SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, abl));
-            SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
-        }
-        // work distribution (SLAT_DYN bits, A/B knob; tickets in d_words[5]): 1 = the batched short-row
-        // tiles, 2 = the rows of the wide launches' window / one-row-hash passes (long, uneven rows:
-        // R-MAT 2^16 A^2 18.0 -> 14.3 ms), 4 = the single-window pass's rows (27k rows take a ticket
-        // each from one word: 30^3 A^6*A numeric 91 -> 383 us). Else a fixed stride over the grid.
-        static const uint32_t kDyn = [] {
-            const char *e = std::getenv("SLAT_DYN");
-            return e ? (uint32_t)std::atoi(e) : 2u;
-        }();
-        unsigned long long *tq = ctx->d_words + 5;
-        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[0], s));
-        if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return failc(st);
-        if (sym_batched) {
-            // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
-            // row's products per tile, listing the rest), then the listed rows by windows
-            unsigned int *lc = (unsigned int *)(ws + o_lc);
-            SLAT_HIPC(hipMemsetAsync(lc, 0, lc_b, s));
-            Args h1 = asym, h2 = asym;
-            h1.cbits = a.cbits;
-            h1.list = h2.list = (uint32_t *)(ws + o_l1);
-            h1.list_cnt = h2.list_cnt = lc;
-            const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kWave - 1) / kWave / wpb + 1, ctx->cu_count * 16ull)));
-            SLAT_HIPC(slat_launch_symbolic_short(idx32, g1, wpb * sym_short_bytes(), s, h1));
-            h2.tq = (kDyn & 2u) ? tq : nullptr;
-            SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
-            a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
-            a.list_cnt = lc + 16;
-        } else if (hash) {
-            Args h1 = asym;
-            h1.tq = (kDyn & 2u) ? tq : nullptr;
-            SLAT_HIPC(slat_launch_symbolic(1, idx32, ell, sym_grid, sym_hash_lds, s, h1));
-            SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h1));
-        } else {
-            SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
-        }
-        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
-        // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
-        const bool bpart = ell && dt != SLAT_F64;
-        if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
-                                   bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
-                                   bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch)))
-            return failc(st);
-        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
-
-        if (exact) {
-            SLAT_HIPC(hipStreamSynchronize(s));
-            const uint64_t total = ctx->h_out[0];
-            C->capacity = std::max<uint64_t>(total, 1);
-            if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
-                slat_dev_alloc(ctx, &C->values, C->capacity * vs, s) != hipSuccess) {
-                slat_csr_free(ctx, C);
-                return fail(ctx, SLAT_EOOM, "C allocation failed");
-            }
-            if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
-        }
-        a.c_col = C->col_idx;
-        a.c_val = C->values;
-        const int win_mode = hash ? 2 : 0;  // numeric instance of the window rows
-        auto launch_num = [&](const Args &x) { return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x); };
-        if (ablate & ~7u) {
-            // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
-            // the real numeric pass below overwrites everything it wrote
-            Args abl = a;
-            abl.ablate = ablate;
-            abl.counts = (uint64_t *)(ws + o_abl);
-            SLAT_HIPC(hipEventRecord(ctx->ev[4], s));
-            SLAT_HIPC(launch_num(abl));
-            SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
-        }
-        if (hash) {
-            Args h1 = a;
-            if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
-            h1.tq = (kDyn & (hash_mode == 3 ? 1u : 2u)) ? tq : nullptr;
-            SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
-        }
-        a.tq = (kDyn & (hash ? 2u : 4u)) ? tq : nullptr;
-        // the window pass is the call's last kernel unless fat rows or the stats copy follow: it stores
-        // the completion word itself (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
-        static const bool kFusedSignal = std::getenv("SLAT_NO_FUSED_SIGNAL") == nullptr;
-        if (kFusedSignal && !fat && !a.stats && wait_mode() == 0) {
-            a.seq = ++ctx->done_seq;
-            a.done = ctx->d_words + 6;
-        }
-        SLAT_HIPC(launch_num(a));
-        if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return failc(st);
     }
+    SLAT_HIPC(launch_num(a));
+    if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return failc(st);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));
     if (a.stats) SLAT_HIPC(hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                              hipMemcpyDeviceToHost, s));
@@ -1055,7 +1034,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     S.nnz = nnz;
     S.flops = flops;
     S.capacity = C->capacity;
-    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u);
+    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;

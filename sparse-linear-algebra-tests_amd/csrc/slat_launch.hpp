@@ -52,7 +52,3 @@ hipError_t slat_launch_symbolic(int mode, bool idx32, bool ell, dim3 grid, size_
                                 const slat::Args &a);
 // the batched short-row symbolic of wide launches (lists the other rows for mode 2)
 hipError_t slat_launch_symbolic_short(bool idx32, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
-// the whole product of a small call in one cooperative kernel (slat_tiny.hip); counts2: the numeric
-// pass's non-zero counts; bar: the grid-barrier counter, target = its value once every block arrived
-hipError_t slat_launch_tiny(int sem, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a, uint64_t *counts2,
-                            unsigned long long *bar, unsigned long long target);

@@ -1443,8 +1443,8 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
 // symbolic): MODE 1 accumulates the rows with <= kHashT / 2 outputs in the LDS hash table and
 // skips the rest, MODE 2 takes the rest by row-span windows.
 // The numeric pass of one wavefront over rows first, first + stride, ... (k_numeric: the grid's
-// waves; k_tiny: the waves of its one workgroup). smem8: the workgroup's LDS, wave wv's region at
-// wv * its size.
+// waves; p.tq: from a ticket queue instead). smem8: the workgroup's LDS, wave wv's region at wv * its
+// size.
 template <typename Sem, typename I, bool ELL, int MODE>
 __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int wv, uint64_t first, uint64_t stride) {
     using S = typename Sem::S;
@@ -2497,9 +2497,14 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
     const int t = threadIdx.x, lane = lane_id(), w = t / kWave;
     const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
     auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    if (t == 0) s_bcast[0] = atomicAdd(ticket, 1ull) - ticket_base;
-    __syncthreads();
-    const uint64_t tile = s_bcast[0];
+    // tiles in ticket order; a grid that is resident at once (ticket = null: at most one block per
+    // CU) takes blockIdx order instead, one memory round trip less
+    uint64_t tile = blockIdx.x;
+    if (ticket) {
+        if (t == 0) s_bcast[0] = atomicAdd(ticket, 1ull) - ticket_base;
+        __syncthreads();
+        tile = s_bcast[0];
+    }
     const uint64_t i0 = tile * kScanTile + (uint64_t)t * kScanItems;
     unsigned long long v[kScanItems], run = 0;
     uint32_t mx = 0;

@@ -13,8 +13,8 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -n 2 $OUT/tests.log
 SLAT_HOST_CLOCK=1 timeout -k 10 300 python tools/host_overhead.py > $OUT/host.txt 2>&1 || { tail -30 $OUT/host.txt; exit 1; }
 tail -5 $OUT/host.txt
-timeout -k 10 600 python tools/bench_protocol.py sweep --threads 16 > $OUT/sweep.csv 2> $OUT/sweep.err || { tail -30 $OUT/sweep.err; exit 1; }
-cat $OUT/sweep.csv
+timeout -k 10 300 python tools/small_cells.py > $OUT/small.csv 2> $OUT/small.err || { tail -30 $OUT/small.err; exit 1; }
+cat $OUT/small.csv
 timeout -k 10 1100 python tools/ab_heavy.py --reps 2 --big --legs c5ord,c5big_ord tree tree:SLAT_NO_FAT_SLICES=1 > $OUT/ab_heavy.txt 2>&1 || { tail -30 $OUT/ab_heavy.txt; exit 1; }
 grep -A4 summary $OUT/ab_heavy.txt
 timeout -k 10 600 python tools/ab.py --reps 2 --c4 --sat64 tree > $OUT/ab.txt 2>&1 || { tail -30 $OUT/ab.txt; exit 1; }
