@@ -425,8 +425,18 @@ static hipError_t launch_compact(dim3 grid, hipStream_t s, const uint64_t *orp, 
 
 // row_ptr[0..n] of a count vector: k_scan_rows (one kernel); the total and the max count land in
 // ctx->h_out[0], [1] once the stream reaches that point
+uint32_t slat_next_scan_epoch(slat_ctx *ctx, hipStream_t s) {
+    if (++ctx->scan_epoch >= (1u << 22)) {  // tag wrap: clear every tagged word once
+        if (ctx->d_status) (void)hipMemsetAsync(ctx->d_status, 0, ctx->status_cap * 8, s);
+        (void)hipMemsetAsync(ctx->d_words + 2, 0, 8, s);
+        ctx->scan_epoch = 1;
+    }
+    return ctx->scan_epoch;
+}
+
 slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s,
-                             const unsigned long long *bpart, uint32_t nbpart, uint32_t vepoch) {
+                             const unsigned long long *bpart, uint32_t nbpart, uint32_t vepoch, const uint32_t *bmax,
+                             uint32_t nbmax) {
     const uint64_t tiles = std::max<uint64_t>((n + kScanTile - 1) / kScanTile, 1);
     if (tiles > ctx->status_cap) {
         if (ctx->d_status) slat_dev_free(ctx, ctx->d_status, s);
@@ -436,15 +446,11 @@ slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, 
         SLAT_HIP(ctx, hipMemsetAsync(ctx->d_status, 0, cap * 8, s));
         ctx->status_cap = cap;
     }
-    if (++ctx->scan_epoch >= (1u << 22)) {  // tag wrap: clear every tagged word once
-        SLAT_HIP(ctx, hipMemsetAsync(ctx->d_status, 0, ctx->status_cap * 8, s));
-        SLAT_HIP(ctx, hipMemsetAsync(ctx->d_words + 2, 0, 8, s));
-        ctx->scan_epoch = 1;
-    }
+    const uint32_t epoch = slat_next_scan_epoch(ctx, s);
     const bool ticketed = tiles > (uint64_t)ctx->cu_count;
     hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status,
-                       ticketed ? ctx->d_words + 1 : nullptr, ctx->ticket_base, ctx->scan_epoch, ctx->d_words + 2,
-                       ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch);
+                       ticketed ? ctx->d_words + 1 : nullptr, ctx->ticket_base, epoch, ctx->d_words + 2,
+                       ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch, bmax, nbmax);
     SLAT_HIP(ctx, hipGetLastError());
     if (ticketed) ctx->ticket_base += tiles;
     return SLAT_OK;
@@ -469,8 +475,11 @@ static void pick_window(uint64_t ncols, uint32_t threads, uint32_t max_ww, uint3
 // End of a call: poll the stream instead of a blocking sync, whose wake-up adds microseconds to
 // every call (SLAT_BLOCKING_SYNC=1 restores the blocking wait)
 // diagnostics (SLAT_HOST_CLOCK=1): host time of each part of a call, printed every 256 calls:
-// [0] checks, workspace and C allocation, [1] enqueueing the kernels, [2] waiting for them, [3] the rest
+// [0] checks and hipSetDevice, [1] launch geometry, [2] workspace, [3] the ELL build's launch, [4] C's
+// allocation, [5] the symbolic launches, [6] the scan / numeric launches, [7] waiting for them,
+// [8] the rest
 struct HostClock {
+    static constexpr int kN = 9;
     static bool on() {
         static const bool e = std::getenv("SLAT_HOST_CLOCK") != nullptr;
         return e;
@@ -481,15 +490,19 @@ struct HostClock {
     }
     void mark(int i) {
         if (!on()) return;
-        static thread_local double acc[4];
+        static thread_local double acc[kN];
+        static thread_local long calls = 0;  // the first 64 calls (one-time costs: code object loads,
+                                             // occupancy queries) are not counted
         const auto now = std::chrono::steady_clock::now();
-        acc[i] += std::chrono::duration<double, std::micro>(now - t).count();
+        if (calls >= 64) acc[i] += std::chrono::duration<double, std::micro>(now - t).count();
         t = now;
-        static thread_local long calls = 0;
-        if (i == 3 && ++calls % 256 == 0) {
-            std::fprintf(stderr, "host us/call: setup %.2f enqueue %.2f wait %.2f finish %.2f\n", acc[0] / 256,
-                         acc[1] / 256, acc[2] / 256, acc[3] / 256);
-            acc[0] = acc[1] = acc[2] = acc[3] = 0;
+        if (i == kN - 1 && ++calls > 64 && (calls - 64) % 256 == 0) {
+            std::fprintf(stderr,
+                         "host us/call: checks %.2f geometry %.2f workspace %.2f ell %.2f alloc %.2f symbolic %.2f "
+                         "scan+numeric %.2f wait %.2f finish %.2f\n",
+                         acc[0] / 256, acc[1] / 256, acc[2] / 256, acc[3] / 256, acc[4] / 256, acc[5] / 256,
+                         acc[6] / 256, acc[7] / 256, acc[8] / 256);
+            for (double &x : acc) x = 0;
         }
     }
 };
@@ -584,6 +597,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         return st;
     }
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    hc.mark(0);
     std::memset(C, 0, sizeof *C);
     std::memset(&ctx->stats, 0, sizeof ctx->stats);
     const uint64_t n = row_end - row_begin;
@@ -719,6 +733,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const bool progress = g_progress.load(std::memory_order_relaxed) != 0;
     const bool timing = (flags & SLAT_FLAG_TIMING) || progress;
 
+    hc.mark(1);
     // workspace: counts [n] | ablation counts [n] | shards | scan temp | ELL cols | ELL vals | ELL groups
     auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t counts_b = up256(n * 8);
@@ -751,7 +766,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
-    if ((st = slat_ensure_ws(ctx, o_fat + fat_b))) return st;
+    const size_t o_bmax = o_fat + fat_b, bmax_b = up256((size_t)sym_grid.x * 4);  // per-block max counts
+    if ((st = slat_ensure_ws(ctx, o_bmax + bmax_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (ell) {
         a.ell_wq = (uint32_t)wq;
@@ -777,6 +793,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     a.host_out = ctx->h_out_dev;
     ctx->h_out[0] = ctx->h_out[1] = ctx->h_out[2] = 0;  // no kernel of this context is in flight
+    hc.mark(2);
     // the ELL image (or B's value summary) first: it runs while the host allocates C and queues
     // the rest, instead of after the host's setup with the GPU idle
     if (ell) {
@@ -801,6 +818,26 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, hipGetLastError());
     }
 
+    // wide launches with B in CSR form: B bucketed by the window passes' column chunk (32 chunks over
+    // the columns, 2^chunk_shift each), so a window walks only its chunks' part of each B row
+    uint32_t *wsplit = nullptr;
+    static const bool kNoWinSplit = std::getenv("SLAT_NO_WIN_SPLIT") != nullptr;  // A/B knob
+    if (hash && !ell && !kNoWinSplit && B->nnz) {
+        uint32_t csh = 0;
+        while (csh < 58 && ((ncols - 1) >> (csh + 5))) ++csh;
+        csh = std::max(csh, 5u);
+        const uint64_t nch1 = ((ncols + (1ull << csh) - 1) >> csh) + 1;
+        if (B->n_rows * nch1 * 4 <= (256ull << 20) &&
+            slat_dev_alloc(ctx, (void **)&wsplit, B->n_rows * nch1 * 4, s) == hipSuccess) {
+            SLAT_HIP(ctx, slat_launch_splits(ctx, B->row_ptr, B->col_idx, B->n_rows, (uint32_t)nch1, csh, wsplit, s));
+            a.wsplit = wsplit;
+            a.wnch1 = (uint32_t)nch1;
+        } else {
+            (void)hipGetLastError();
+            wsplit = nullptr;
+        }
+    }
+    hc.mark(3);
     // capacity by exact bound (no mid-call sync) unless it exceeds the budget
     unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
     const unsigned __int128 dense = (unsigned __int128)n * ncols;
@@ -835,6 +872,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     auto failc = [&](slat_status e) {
         (void)hipStreamSynchronize(s);
         slat_csr_free(ctx, C);
+        if (wsplit) slat_dev_free(ctx, wsplit, s);
         return e;
     };
 #define SLAT_HIPC(expr)                                                                            \
@@ -846,7 +884,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         }                                                                                          \
     } while (0)
 
-    hc.mark(0);
+    hc.mark(4);
     if (a.stats || SLAT_PHASES) SLAT_HIPC(hipMemsetAsync(a.shards, 0, shards_b, s));
     asym.counts = a.counts;
     asym.shards = a.shards;
@@ -858,6 +896,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     asym.sbm = a.sbm;
     asym.smask = a.smask;
     asym.nblk = a.nblk;
+    asym.wsplit = a.wsplit;
+    asym.wnch1 = a.wnch1;
     hipError_t e;
     slat::FatArgs fat_args = {};
     slat::FatArgs *fa = &fat_args;
@@ -875,10 +915,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, abl));
         SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
     }
-    // work distribution (SLAT_DYN bits, A/B knob; tickets in d_words[5]): 1 = the batched short-row
-    // tiles, 2 = the rows of the wide launches' window / one-row-hash passes (long, uneven rows:
-    // R-MAT 2^16 A^2 18.0 -> 14.3 ms), 4 = the single-window pass's rows (27k rows take a ticket
-    // each from one word: 30^3 A^6*A numeric 91 -> 383 us). Else a fixed stride over the grid.
+    // work distribution (tickets in d_words[5]): the rows of the wide launches' window / one-row-hash
+    // passes (long, uneven rows: R-MAT 2^16 A^2 18.0 -> 15.3 ms); the single-window pass and the
+    // short-row tiles keep a fixed stride (tickets measured slower there).
+    // SLAT_DYN=0: no tickets (A/B knob)
     static const uint32_t kDyn = [] {
         const char *e = std::getenv("SLAT_DYN");
         return e ? (uint32_t)std::atoi(e) : 2u;
@@ -907,14 +947,18 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIPC(slat_launch_symbolic(1, idx32, ell, sym_grid, sym_hash_lds, s, h1));
         SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h1));
     } else {
+        // single-window launch without fat rows: symbolic leaves per-block max row counts for the
+        // scan's last tile (<= 16 per scan thread)
+        if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
         SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
     }
+    hc.mark(5);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
     // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
     const bool bpart = ell && dt != SLAT_F64;
     if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
                                bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
-                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch)))
+                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch, asym.bmax, sym_grid.x)))
         return failc(st);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
 
@@ -946,10 +990,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (hash) {
         Args h1 = a;
         if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
-        h1.tq = (kDyn & (hash_mode == 3 ? 1u : 2u)) ? tq : nullptr;
+        h1.tq = (kDyn & 2u) && hash_mode != 3 ? tq : nullptr;
         SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
     }
-    a.tq = (kDyn & (hash ? 2u : 4u)) ? tq : nullptr;
+    a.tq = (kDyn & 2u) && hash ? tq : nullptr;
     // the window pass is the call's last kernel unless fat rows or the stats copy follow: it stores
     // the completion word itself (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
     static const bool kFusedSignal = std::getenv("SLAT_NO_FUSED_SIGNAL") == nullptr;
@@ -958,14 +1002,15 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         a.done = ctx->d_words + 6;
     }
     SLAT_HIPC(launch_num(a));
+    if (wsplit) slat_dev_free(ctx, wsplit, s);  // stream-ordered: reused only by later work
     if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return failc(st);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));
     if (a.stats) SLAT_HIPC(hipMemcpyAsync(ctx->h_shards, a.shards, sizeof(unsigned long long) * kShards * kShardStride,
                                              hipMemcpyDeviceToHost, s));
-    hc.mark(1);
+    hc.mark(6);
     SLAT_HIPC(wait_stream(ctx, s, a.seq));
 #undef SLAT_HIPC
-    hc.mark(2);
+    hc.mark(7);
     if (SLAT_PHASES) {
         // diagnostic build: per-phase cycles of the numeric kernel, summed over waves
         unsigned long long ph[kPhaseSlots * 64];
@@ -1060,7 +1105,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         std::fprintf(stderr, "\r  symbolic: done in %.1fs (%.0f rows/s)                    \n", ts, rows / std::max(ts, 1e-9));
         std::fprintf(stderr, "\r  numeric:  done in %.1fs (%.0f rows/s)                    \n", tn, rows / std::max(tn, 1e-9));
     }
-    hc.mark(3);
+    hc.mark(8);
     return SLAT_OK;
 }
 

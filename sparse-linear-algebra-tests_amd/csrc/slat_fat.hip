@@ -45,9 +45,11 @@ template <typename Sem>
 __host__ __device__ constexpr uint32_t fr_chunk() {
     return (128u * 1024u) / (uint32_t)(sizeof(typename Sem::V) * Sem::kSlots);
 }
+constexpr uint32_t kMaxBuckets = 256;  // accumulator chunks a bucketed row may span (LDS counters)
 template <typename Sem>
 __host__ __device__ constexpr size_t fr_lds() {
-    return (size_t)fr_chunk<Sem>() * sizeof(typename Sem::V) * Sem::kSlots + fr_chunk<Sem>() / 8 + 64 * 8;
+    return (size_t)fr_chunk<Sem>() * sizeof(typename Sem::V) * Sem::kSlots + fr_chunk<Sem>() / 8 + 64 * 8 +
+           (Sem::kOrdered ? 0 : 2 * kMaxBuckets * 4);
 }
 
 __device__ __forceinline__ uint32_t cap63(uint64_t x) { return x < 63 ? (uint32_t)x : 63u; }
@@ -400,6 +402,56 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
     }
 }
 
+// MAGNUS's long-row category with the products bucketed: one walk counts each accumulator chunk's
+// products, a second writes them (column, product) into the chunk's bucket in the block's global
+// region, and each chunk then accumulates from its bucket alone. Two walks of the row instead of one
+// per touched chunk, each of which pays every A entry's B-row bounds again (a hub row touching 16
+// chunks walked 16 times), for one write and one read of the products. Returns false (nothing
+// written) when the row's products outgrow the block's region.
+template <typename Sem, typename I, typename Emit>
+__device__ __forceinline__ bool fr_bucketed(const FatArgs &f, I a0, I a1, uint32_t nbk, uint32_t *bcnt, uint32_t *boff,
+                                            typename Sem::V *acc, uint32_t *bits, uint32_t *sh, Emit &&emit) {
+    using S = typename Sem::S;
+    using P = typename Sem::P;
+    constexpr uint32_t CH = fr_chunk<Sem>();
+    constexpr uint32_t csh = __builtin_ctz(CH);
+    const Args &p = f.a;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t c = t; c < nbk; c += kFB) bcnt[c] = 0;
+    __syncthreads();
+    fr_walk<S, false, I>(p, a0, a1, 0u, (uint32_t)p.ncols, true, [&](uint32_t c, S, S) { atomicAdd(&bcnt[c >> csh], 1u); });
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(t < nbk ? bcnt[t] : 0u, sh, tot);
+    if (tot > f.bcap) return false;  // block-uniform
+    if (t < nbk) {
+        boff[t] = ex;
+        bcnt[t] = ex;  // from here the chunk's write cursor
+    }
+    __syncthreads();
+    uint32_t *bc = f.bcol + (uint64_t)blockIdx.x * f.bcap;
+    P *bv = (P *)f.bval + (uint64_t)blockIdx.x * f.bcap;
+    fr_walk<S, true, I>(p, a0, a1, 0u, (uint32_t)p.ncols, true, [&](uint32_t c, S a, S b) {
+        const uint32_t at = atomicAdd(&bcnt[c >> csh], 1u);
+        bc[at] = c;
+        bv[at] = Sem::prod(a, b);
+    });
+    __syncthreads();
+    for (uint32_t k = 0; k < nbk; ++k) {
+        const uint32_t s0 = boff[k], s1 = k + 1 < nbk ? boff[k + 1] : tot;
+        if (s0 == s1) continue;  // block-uniform
+        const uint32_t c0 = k << csh;
+        for (uint32_t i = s0 + t; i < s1; i += kFB) {
+            const uint32_t o = bc[i] - c0;
+            Sem::acc(acc, o, bv[i]);
+            atomicOr(&bits[o >> 5], 1u << (o & 31));
+        }
+        __syncthreads();
+        emit(c0);
+    }
+    return true;
+}
+
 template <typename Sem, typename I>
 __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
     using S = typename Sem::S;
@@ -411,11 +463,13 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
     V *acc = (V *)smem;
     uint32_t *bits = (uint32_t *)(smem + (size_t)CH * sizeof(V) * Sem::kSlots);
     uint32_t *sh = bits + kWords;
+    uint32_t *bcnt = sh + 128, *boff = bcnt + kMaxBuckets;  // (bucketed rows; past the scan words)
     for (uint32_t w = threadIdx.x; w < CH * Sem::kSlots; w += kFB) acc[w] = V(0);
     for (uint32_t w = threadIdx.x; w < kWords; w += kFB) bits[w] = 0;
     __syncthreads();
     S *cval = (S *)p.c_val;
     const unsigned int nl = *(volatile unsigned int *)f.cnt;
+    const uint32_t nbk = (uint32_t)((p.ncols + CH - 1) / CH);
     uint32_t zrows = 0;
     for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
         const uint64_t row = f.list[li];
@@ -424,13 +478,9 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
         const unsigned long long cm = f.cmask[li];
         uint64_t pos = 0;
         uint32_t zeros = 0;
-        for (uint64_t c0 = 0; c0 < p.ncols; c0 += CH) {
-            // skip chunks with no product (mask granule 2^csh columns, a multiple of CH or the last)
-            if (!((cm >> cap63(c0 >> f.csh)) & 1ull)) continue;
-            const uint32_t c1 = (uint32_t)min<uint64_t>(p.ncols, c0 + CH);
-            fr_accumulate<Sem, I>(f, a0, a1, (uint32_t)c0, c1, acc, bits);
-            __syncthreads();
-            // emit: thread t owns bitmap word t (32 columns); positions by a block scan
+        // emit of the chunk at c0 from the accumulator: thread t owns bitmap word t (32 columns),
+        // positions by a block scan; leaves the accumulator and bitmap clear
+        auto emit = [&](uint32_t c0) {
             uint32_t x = 0;
             if (threadIdx.x < kWords) x = bits[threadIdx.x];
             uint32_t tot;
@@ -444,13 +494,28 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
                 zeros += Sem::is_zero(v) ? 1u : 0u;
                 const uint64_t at = ob + pos + pre + q;
                 if (at < oe) {  // never write past the row's slice
-                    p.c_col[at] = (uint32_t)c0 + o;
+                    p.c_col[at] = c0 + o;
                     cval[at] = v;
                 }
             }
             if (threadIdx.x < kWords) bits[threadIdx.x] = 0;
             pos += tot;
             __syncthreads();
+        };
+        bool done = false;
+        if constexpr (!Sem::kOrdered)
+            // bucketed when the row spans 3 or more chunks (fewer: the re-walks cost no more)
+            if (f.bcol && nbk <= kMaxBuckets && __popcll(cm) >= 3)
+                done = fr_bucketed<Sem, I>(f, a0, a1, nbk, bcnt, boff, acc, bits, sh, emit);
+        if (!done) {
+            for (uint64_t c0 = 0; c0 < p.ncols; c0 += CH) {
+                // skip chunks with no product (mask granule 2^csh columns, a multiple of CH or the last)
+                if (!((cm >> cap63(c0 >> f.csh)) & 1ull)) continue;
+                const uint32_t c1 = (uint32_t)min<uint64_t>(p.ncols, c0 + CH);
+                fr_accumulate<Sem, I>(f, a0, a1, (uint32_t)c0, c1, acc, bits);
+                __syncthreads();
+                emit((uint32_t)c0);
+            }
         }
         uint32_t zt;
         (void)block_excl_scan(zeros, sh, zt);
@@ -469,6 +534,14 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
 using namespace slat;
 
 // workspace bytes of the fat-row category for n rows
+hipError_t slat_launch_splits(slat_ctx *ctx, const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb, uint32_t nch1,
+                              uint32_t shift, uint32_t *split, hipStream_t s) {
+    const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb * nch1 + kBlock - 1) / kBlock,
+                                                                           (uint64_t)ctx->cu_count * 16));
+    hipLaunchKernelGGL(k_fr_splits, dim3(gs), dim3(kBlock), 0, s, b_rp, b_col, nb, nch1, shift, split);
+    return hipGetLastError();
+}
+
 size_t slat_fat_ws(uint64_t n) { return ((n + 255) & ~255ull) * (1 + 4 + 8) + 256; }
 
 // Select the fat rows (marks into a.fr_mark's buffer) and count them on the device; nothing to do on
@@ -491,6 +564,9 @@ slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
     f.split = nullptr;
     f.nch1 = 0;
     f.gsh = 0;
+    f.bcol = nullptr;
+    f.bval = nullptr;
+    f.bcap = 0;
     SLAT_HIP(ctx, hipMemsetAsync(f.cnt, 0, 4, s));
     a.fr_mark = f.mark;
     f.a = a;
@@ -567,6 +643,27 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
             (void)hipGetLastError();
         }
     }
+    // product buckets (not for the fold order): bcap pairs per block, dropped when the memory is not there
+    uint32_t *bcol = nullptr;
+    void *bval = nullptr;
+    h.bcol = nullptr;
+    h.bval = nullptr;
+    h.bcap = 0;
+    static const bool kNoBuckets = std::getenv("SLAT_NO_FAT_BUCKETS") != nullptr;  // A/B knob
+    if (!Sem::kOrdered && !kNoBuckets && (h.a.ncols + fr_chunk<Sem>() - 1) / fr_chunk<Sem>() <= kMaxBuckets) {
+        const uint32_t cap = 1u << 19;
+        const size_t nbk = (size_t)g.x * cap;
+        if (slat_dev_alloc(ctx, (void **)&bcol, nbk * 4, ctx->stream) == hipSuccess &&
+            slat_dev_alloc(ctx, &bval, nbk * sizeof(typename Sem::P), ctx->stream) == hipSuccess) {
+            h.bcol = bcol;
+            h.bval = bval;
+            h.bcap = cap;
+        } else {
+            (void)hipGetLastError();
+            if (bcol) slat_dev_free(ctx, bcol, ctx->stream);
+            bcol = nullptr;
+        }
+    }
     static std::atomic<uint64_t> attr{0};  // per device, as above
     if (!(attr.load(std::memory_order_relaxed) >> (ctx->device & 63) & 1)) {  // > 64 KB of dynamic LDS per block
         (void)hipFuncSetAttribute((const void *)k_fr_numeric<Sem, uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -579,6 +676,8 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
         hipLaunchKernelGGL((k_fr_numeric<Sem, uint64_t>), g, dim3(kFB), lds, ctx->stream, h);
     const hipError_t e = hipGetLastError();
     if (split) slat_dev_free(ctx, split, ctx->stream);  // stream-ordered: reused only by later work
+    if (bcol) slat_dev_free(ctx, bcol, ctx->stream);
+    if (bval) slat_dev_free(ctx, bval, ctx->stream);
     return e;
 }
 

@@ -20,9 +20,18 @@ struct FatArgs {
     const uint32_t *split;
     uint32_t nch1;
     uint32_t gsh;
+    // products bucketed by accumulator chunk (integer semirings and f64 in any order; null = none):
+    // each block's region of bcap (column, product) pairs at bcol / bval + blockIdx.x * bcap
+    uint32_t *bcol;
+    void *bval;
+    uint32_t bcap;
 };
 }  // namespace slat
 
+// B (CSR) bucketed by column granule of 2^shift columns on stream s: split[k * nch1 + g] = the offset
+// in B row k of its first column >= g << shift, g in [0, nch1) (the last = the row's length)
+hipError_t slat_launch_splits(slat_ctx *ctx, const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb, uint32_t nch1,
+                              uint32_t shift, uint32_t *split, hipStream_t s);
 // workspace bytes of the category for n rows
 size_t slat_fat_ws(uint64_t n);
 // mark and list the rows of >= 16384 products (sets a.fr_mark); nothing comes back to the host

@@ -109,8 +109,13 @@ slat_status slat_check_view(slat_ctx *ctx, const slat_csr_view *v, const char *n
 // rp[0..n] = exclusive prefix of counts[0..n) (rp[n] = total) by k_scan_rows on stream s; the total
 // and the max count land in ctx->h_out[0], [1] once the stream reaches that point
 // bpart / nbpart / vepoch: k_build_ell's u32 B-value partials, reduced into ctx->d_vmax (else none)
+// bmax / nbmax (<= 4096): per-block max counts left by the counts' producer; the scan then reduces
+// those instead of its tiles' (slat_next_scan_epoch: the epoch the next scan tags its words with; it
+// clears them on wrap)
 slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s,
-                             const unsigned long long *bpart = nullptr, uint32_t nbpart = 0, uint32_t vepoch = 0);
+                             const unsigned long long *bpart = nullptr, uint32_t nbpart = 0, uint32_t vepoch = 0,
+                             const uint32_t *bmax = nullptr, uint32_t nbmax = 0);
+uint32_t slat_next_scan_epoch(slat_ctx *ctx, hipStream_t s);
 
 // StdRng stream position (host_gen.cpp): key words and the index of the next keystream word; and
 // the host state after `draws` more u64 draws (device generators draw by position)

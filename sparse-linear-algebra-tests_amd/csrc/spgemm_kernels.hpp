@@ -115,12 +115,20 @@ struct Args {
     // rows of the fat-row category (slat_fat.hip: a workgroup and a dense LDS accumulator per row),
     // which the kernels here skip; null = none
     const uint8_t *fr_mark;
-    // rows (k_symbolic, k_numeric) or row tiles (k_numeric_short) from a ticket counter instead of
-    // a fixed stride over the grid (null)
+    // rows of the wide launches' window / hash passes (k_symbolic, k_numeric MODE 1 / 2) from a
+    // ticket counter instead of a fixed stride over the grid (null)
     unsigned long long *tq;
     // the call's completion (seq != 0: this launch is the call's last kernel; signal_done)
     unsigned long long *done;
     unsigned long long seq;
+    // k_symbolic (single-window launches): each block's max row count at bmax[blockIdx.x], so the
+    // scan that follows need not reduce it across its tiles (null: the scan does)
+    uint32_t *bmax;
+    // B (CSR form) bucketed by column chunk of the wide launches' window passes: wsplit[k * wnch1 + g]
+    // = the offset in B row k of its first column >= g << chunk_shift(ncols) (null: none). A window
+    // walks only its chunks' part of each B row instead of the whole row with a column filter
+    const uint32_t *wsplit;
+    uint32_t wnch1;
 };
 
 __device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.fr_mark && p.fr_mark[row]; }
@@ -615,8 +623,10 @@ __device__ __forceinline__ void walk_brow(const Args &p, uint32_t k, typename Se
 // walked by its own lane, a longer one by the whole wave (lanes over its columns), so no lane walks
 // thousands of entries alone (power-law B rows).
 constexpr uint32_t kLongB = 32;
+// [g0, g1) (g1 > 0): only the B entries of those column chunks (p.wsplit)
 template <typename Sem, bool VALS, typename I, int N, typename G>
-__device__ __forceinline__ void walk_csr(const Args &p, const uint32_t *k, const typename Sem::S *a, G &&grp) {
+__device__ __forceinline__ void walk_csr(const Args &p, const uint32_t *k, const typename Sem::S *a, G &&grp,
+                                         uint32_t g0 = 0, uint32_t g1 = 0) {
     using S = typename Sem::S;
     const int lane = lane_id();
     const S *bv_ = (const S *)p.b_val;
@@ -625,8 +635,15 @@ __device__ __forceinline__ void walk_csr(const Args &p, const uint32_t *k, const
         bs[Q] = 0;
         be[Q] = 0;
         if (k[Q] < p.b_nrows) {
-            bs[Q] = (I)p.b_rp[k[Q]];
-            be[Q] = (I)p.b_rp[k[Q] + 1];
+            if (g1) {
+                const I r = (I)p.b_rp[k[Q]];
+                const uint32_t *sp = p.wsplit + (uint64_t)k[Q] * p.wnch1;
+                bs[Q] = r + (I)sp[g0];
+                be[Q] = r + (I)sp[g1];
+            } else {
+                bs[Q] = (I)p.b_rp[k[Q]];
+                be[Q] = (I)p.b_rp[k[Q] + 1];
+            }
         }
     });
     sfor<N>([&](auto Q) {
@@ -647,7 +664,7 @@ __device__ __forceinline__ void walk_csr(const Args &p, const uint32_t *k, const
 
 // Lane-per-A-entry walk of a row: lane l owns entries base + l and base + 64 + l.
 template <typename Sem, bool ELL, bool VALS, typename I, typename G>
-__device__ __forceinline__ void walk_row(const Args &p, I a0, I a1, G &&grp) {
+__device__ __forceinline__ void walk_row(const Args &p, I a0, I a1, G &&grp, uint32_t g0 = 0, uint32_t g1 = 0) {
     using S = typename Sem::S;
     const int lane = lane_id();
     const S *av_ = (const S *)p.a_val;
@@ -667,7 +684,7 @@ __device__ __forceinline__ void walk_row(const Args &p, I a0, I a1, G &&grp) {
             if (kk[0] < p.b_nrows) walk_brow<Sem, ELL, VALS, I>(p, kk[0], av[0], 0, grp);
             if (kk[1] < p.b_nrows) walk_brow<Sem, ELL, VALS, I>(p, kk[1], av[1], 0, grp);
         } else {
-            walk_csr<Sem, VALS, I, 2>(p, kk, av, grp);
+            walk_csr<Sem, VALS, I, 2>(p, kk, av, grp, g0, g1);
         }
     }
 }
@@ -992,6 +1009,7 @@ struct RowWalker {
     uint32_t bk0 = kSent, bk1 = kSent, bt0 = 0, bt1 = 0, nb = 0;
     S ba0 = S(0), ba1 = S(0);
     uint32_t amax = 0;  // lane max of the A values seen (narrow-slot bound, u32)
+    uint32_t sg0 = 0, sg1 = 0;  // CSR B: walk only column chunks [sg0, sg1) of each B row (p.wsplit)
 
     __device__ __forceinline__ RowWalker(const Args &p_, I a0_, I a1_) : p(p_), a0(a0_), a1(a1_) {
         len = (uint64_t)(a1 - a0);
@@ -1120,9 +1138,9 @@ struct RowWalker {
                 if (nb > 1) grp(ct1, pt1);
             }
         } else if (single) {
-            walk_csr<Sem, VV, I, kRegQ>(p, kq, aq, grp);
+            walk_csr<Sem, VV, I, kRegQ>(p, kq, aq, grp, sg0, sg1);
         } else {
-            walk_row<Sem, false, VV, I>(p, a0, a1, grp);
+            walk_row<Sem, false, VV, I>(p, a0, a1, grp, sg0, sg1);
         }
     }
 };
@@ -1384,7 +1402,14 @@ __device__ __forceinline__ uint64_t sym_row(const Args &p, uint64_t row, bool li
         if (!p.wide) {
             window(std::true_type{}, 0u);
         } else if constexpr (MODE == 2) {
-            for_windows(lo, hi, WIN, cmask, csh, [&](uint32_t wlo) { window(std::false_type{}, wlo); });
+            for_windows(lo, hi, WIN, cmask, csh, [&](uint32_t wlo) {
+                // CSR B bucketed by chunk: the window walks only its chunks' part of each B row
+                if (!ELL && p.wsplit) {
+                    rw.sg0 = wlo >> csh;
+                    rw.sg1 = (uint32_t)min<uint64_t>(p.wnch1 - 1, (((uint64_t)wlo + WIN - 1) >> csh) + 1);
+                }
+                window(std::false_type{}, wlo);
+            });
         } else {
             for (uint64_t wlo = lo & ~31ull; wlo <= hi; wlo += WIN) window(std::false_type{}, (uint32_t)wlo);
         }
@@ -1392,8 +1417,16 @@ __device__ __forceinline__ uint64_t sym_row(const Args &p, uint64_t row, bool li
     return cnt;
 }
 
+// variant builds: -DSLAT_SYM_WPE=w caps k_symbolic's registers for w waves per SIMD (0: no cap)
+#ifndef SLAT_SYM_WPE
+#define SLAT_SYM_WPE 0
+#endif
 template <typename I, bool ELL, int MODE = 0>
-__global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
+__global__ __launch_bounds__(kBlock)
+#if SLAT_SYM_WPE
+__attribute__((amdgpu_waves_per_eu(SLAT_SYM_WPE)))
+#endif
+void k_symbolic(Args p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     constexpr int kWpb = kBlock / kWave;
     const int lane = lane_id();
@@ -1408,13 +1441,23 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
             p.shards[threadIdx.x * kShardStride + 2] = 0;
         }
     }
+    // the block's max row count (p.bmax): LDS max of the waves' maxima; the last wave to finish
+    // stores it (no block barrier at the end, no global atomics on one word)
+    __shared__ uint32_t s_bmax, s_bdone;
+    if (p.bmax) {
+        if (threadIdx.x == 0) s_bmax = s_bdone = 0;
+        __syncthreads();
+    }
     for (uint32_t w = lane; w < region_w; w += kWave) L0[w] = MODE == 1 ? kSent : 0u;
     wave_sync();
     unsigned long long flops = 0;
+    uint64_t mx = 0;  // max row count (p.bmax)
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
-    const bool dyn = p.tq != nullptr;  // launch-uniform
+    // tickets only in the wide launches' passes (MODE 1 / 2): the code costs the single-window
+    // instance 18 VGPRs even unused
+    const bool dyn = MODE != 0 && p.tq != nullptr;  // launch-uniform
     const TicketQueue tq(p.tq, nit, stride);
     unsigned long long pend = 0;
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
@@ -1424,9 +1467,14 @@ __global__ __launch_bounds__(kBlock) void k_symbolic(Args p) {
         const uint64_t cnt = sym_row<I, ELL, MODE>(p, row, listed, L0, flops);
         if (cnt == kNoRow) continue;
         if (lane == 0) p.counts[row] = cnt;
+        mx = max(mx, cnt);
     }
     if (p.stats && lane == 0 && flops)
         atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
+    if (p.bmax && lane == 0) {
+        atomicMax(&s_bmax, (uint32_t)(mx < 0xFFFFFFFFull ? mx : 0xFFFFFFFFull));
+        if (atomicAdd(&s_bdone, 1u) == (uint32_t)kWpb - 1) p.bmax[blockIdx.x] = atomicMax(&s_bmax, 0u);
+    }
 }
 
 // k_numeric's register cap: 3 waves per SIMD (<= 168 VGPRs). The wide-slot (Sat64 / f64) and
@@ -1502,7 +1550,7 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
     const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     using RW = RowWalker<Sem, I, ELL, kVals>;
-    const bool dyn = p.tq != nullptr;  // launch-uniform
+    const bool dyn = MODE != 0 && p.tq != nullptr;  // launch-uniform (single-window passes: a fixed stride)
     const TicketQueue tq(p.tq, nit, stride);
     unsigned long long pend = 0;
     for (uint64_t it = first; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
@@ -1806,7 +1854,14 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
             if (!p.wide) {
                 window(std::true_type{}, 0u);
             } else if constexpr (MODE == 2) {
-                for_windows(lo, hi, WIN, cmask, csh, [&](uint32_t wlo) { window(std::false_type{}, wlo); });
+                for_windows(lo, hi, WIN, cmask, csh, [&](uint32_t wlo) {
+                // CSR B bucketed by chunk: the window walks only its chunks' part of each B row
+                if (!ELL && p.wsplit) {
+                    rw.sg0 = wlo >> csh;
+                    rw.sg1 = (uint32_t)min<uint64_t>(p.wnch1 - 1, (((uint64_t)wlo + WIN - 1) >> csh) + 1);
+                }
+                window(std::false_type{}, wlo);
+            });
             } else {
                 for (uint64_t wlo64 = lo & ~31ull; wlo64 <= hi; wlo64 += WIN) window(std::false_type{}, (uint32_t)wlo64);
             }
@@ -2262,14 +2317,8 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
     const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
     PhaseClock pc{};  // diagnostic builds (SLAT_PHASES): where the waves' time goes
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
-    const bool dyn = p.tq != nullptr;  // launch-uniform
-    const TicketQueue tq(p.tq, ntiles, (uint64_t)gridDim.x * kWpb);
     const XcdStride xs(ntiles, kWpb, wv);
-    unsigned long long pend = 0;
-    const uint64_t tend = dyn ? ntiles : xs.end;
-    for (uint64_t tile = dyn ? (uint64_t)blockIdx.x * kWpb + wv : xs.first; tile < tend;
-         tile = dyn ? tq.resolve(pend) : tile + xs.stride) {
-        if (dyn) pend = tq.issue();
+    for (uint64_t tile = xs.first; tile < xs.end; tile += xs.stride) {
         const uint64_t r0 = tile * kWave, r = r0 + lane;
         const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
         uint64_t A0j = 0, A1j = 0, obj = 0, oej = 0;
@@ -2490,7 +2539,8 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
                                                             unsigned long long ticket_base, uint32_t epoch,
                                                             unsigned long long *maxw, unsigned long long *host_out,
                                                             const unsigned long long *bpart, uint32_t nbpart,
-                                                            unsigned long long *vmax, uint32_t vepoch) {
+                                                            unsigned long long *vmax, uint32_t vepoch,
+                                                            const uint32_t *bmax, uint32_t nbmax) {
     __shared__ unsigned long long wsum[kScanThreads / kWave];
     __shared__ unsigned long long s_bcast[2];
     __shared__ uint32_t wmax[kScanThreads / kWave];
@@ -2505,6 +2555,19 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
         __syncthreads();
         tile = s_bcast[0];
     }
+    // bmax (<= 16 * kScanThreads entries): the counts' producer left per-block max counts; the last
+    // tile reduces them, its loads issued now so they land during the look-back
+    uint32_t bm = 0;
+    if (bmax && tile == ntiles - 1) {
+        uint32_t q[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t i = (uint32_t)t + (uint32_t)k * kScanThreads;
+            q[k] = i < nbmax ? bmax[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) bm = max(bm, q[k]);
+    }
     const uint64_t i0 = tile * kScanTile + (uint64_t)t * kScanItems;
     unsigned long long v[kScanItems], run = 0;
     uint32_t mx = 0;
@@ -2517,7 +2580,7 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
         v[e] = run;
     }
     const unsigned long long wi = wave_incl_scan_u64(run);
-    mx = wave_max_u32(mx);
+    mx = wave_max_u32(bmax ? bm : mx);
     if (lane == kWave - 1) wsum[w] = wi;
     if (lane == 0) wmax[w] = mx;
     __syncthreads();
@@ -2531,14 +2594,15 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
         uint32_t m = 0;
         for (int k = 0; k < kScanThreads / kWave; ++k) m = max(m, wmax[k]);
         // max row first (its result waited for), then the status: the max is in place once any
-        // later tile sees this tile's status
-        pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
+        // later tile sees this tile's status (bmax: the last tile has it from the producer's maxima)
+        if (!bmax) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
         const unsigned long long excl = lookback_prefix(status, tile, epoch, agg);
         s_bcast[1] = excl;
         if (tile == ntiles - 1) {
             if (n > 0) rp[0] = 0;
-            const unsigned long long mw = ld(maxw);
-            const unsigned long long out[2] = {excl + agg, (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull};
+            const unsigned long long mw = bmax ? 0ull : ld(maxw);
+            const unsigned long long out[2] = {excl + agg, bmax ? (unsigned long long)m
+                                                                : (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull};
             for (int k = 0; k < 2; ++k)
                 __hip_atomic_store(&host_out[k], out[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
