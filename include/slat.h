@@ -74,6 +74,9 @@ typedef enum { SLAT_DEVICE = 0, SLAT_HOST = 1 } slat_residency;
 /* the 64-bit-offset kernel instances even when every offset fits 32 bits (they run by themselves
  * once nnz(A) or nnz(B) reaches 2^32; the flag lets small inputs test them) */
 #define SLAT_FLAG_IDX64 0x10u
+/* the regular multi-kernel pipeline even for a small product (which otherwise runs as one kernel,
+ * slat_tiny.hip); results are identical either way (tests run both) */
+#define SLAT_FLAG_NO_TINY 0x20u
 
 typedef struct slat_ctx slat_ctx;
 
@@ -112,7 +115,7 @@ typedef struct {
     double numeric_ms;
     double compact_ms;
     double total_ms;       /* first event to last event on the stream */
-    uint32_t mode;         /* bits: 1 = 32-bit offsets, 2 = B's ELL image */
+    uint32_t mode;         /* bits: 1 = 32-bit offsets, 2 = B's ELL image, 4 = the one-kernel small path */
     uint32_t window_words; /* LDS bitmap words per window */
     uint32_t exact_alloc;  /* 1 if the mid-call-sync path was taken */
     uint32_t dropped_rows; /* rows that lost explicit zeros in the numeric pass */

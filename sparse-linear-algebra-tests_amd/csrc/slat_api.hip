@@ -434,10 +434,8 @@ uint32_t slat_next_scan_epoch(slat_ctx *ctx, hipStream_t s) {
     return ctx->scan_epoch;
 }
 
-slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s,
-                             const unsigned long long *bpart, uint32_t nbpart, uint32_t vepoch, const uint32_t *bmax,
-                             uint32_t nbmax) {
-    const uint64_t tiles = std::max<uint64_t>((n + kScanTile - 1) / kScanTile, 1);
+// the look-back status words for `tiles` tiles (k_scan_rows, k_tiny)
+static slat_status ensure_status(slat_ctx *ctx, uint64_t tiles, hipStream_t s) {
     if (tiles > ctx->status_cap) {
         if (ctx->d_status) slat_dev_free(ctx, ctx->d_status, s);
         ctx->d_status = nullptr;
@@ -446,6 +444,15 @@ slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, 
         SLAT_HIP(ctx, hipMemsetAsync(ctx->d_status, 0, cap * 8, s));
         ctx->status_cap = cap;
     }
+    return SLAT_OK;
+}
+
+slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s,
+                             const unsigned long long *bpart, uint32_t nbpart, uint32_t vepoch, const uint32_t *bmax,
+                             uint32_t nbmax) {
+    const uint64_t tiles = std::max<uint64_t>((n + kScanTile - 1) / kScanTile, 1);
+    slat_status st;
+    if ((st = ensure_status(ctx, tiles, s))) return st;
     const uint32_t epoch = slat_next_scan_epoch(ctx, s);
     const bool ticketed = tiles > (uint64_t)ctx->cu_count;
     hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status,
@@ -675,10 +682,21 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // padded ELL copy of B when its rows are short (bounded blow-up)
     const uint64_t wq = (maxrow_b + 3) / 4;
     const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
+    // small products: the whole call in one regular launch (slat_tiny.hip) — one window of at most
+    // 8192 columns, <= 2048 rows (at 3375 rows, the 15^3 cells, it measured 1-2 us slower than the
+    // pipeline: profiles/r03_small_cells_tiny_abi.csv), 32-bit offsets, a wave per row with every row in flight, a product bound a wave
+    // finishes in microseconds, no fat rows, and no per-pass timing or stats (those report the
+    // regular pipeline's passes)
+    static const bool kNoTiny = std::getenv("SLAT_NO_TINY") != nullptr;
+    const bool tiny = !kNoTiny && !asym.wide && ncols <= 8192 && n <= 2048 && idx32 && wait_mode() == 0 && !ablate &&
+                      !(flags & (SLAT_FLAG_TIMING | SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) &&
+                      g_progress.load(std::memory_order_relaxed) == 0 &&
+                      (unsigned __int128)a_nnz_block * maxrow_b <= (1u << 18) &&
+                      (A->max_row_nnz ? (unsigned __int128)A->max_row_nnz * maxrow_b < 16384 : maxrow_b <= 32);
     static const bool kNoEll = std::getenv("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
-                     !kNoEll;  // 24-bit row index, 31-bit byte offsets in the kernels
+                     !kNoEll && !tiny;  // 24-bit row index, 31-bit byte offsets in the kernels
 
     // LDS sizing and grids. The numeric grid is the kernel's resident capacity (waves stride over
     // rows; measured faster than oversubscribing); symbolic takes up to 16 blocks per CU.
@@ -751,7 +769,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
     static const bool kNoSbm = std::getenv("SLAT_NO_SBM") != nullptr;
-    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm;
+    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny;
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
@@ -762,7 +780,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // max row of A x max row of B (A's max row unknown: when B has long rows)
     static const bool kNoFat = std::getenv("SLAT_NO_FAT") != nullptr;
     const uint64_t maxrow_a = A->max_row_nnz;
-    const bool fat = !kNoFat && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
+    const bool fat = !kNoFat && !tiny && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= 16384 : maxrow_b > 32);
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
@@ -778,7 +796,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             a.b_vmax = ctx->d_vmax;
             a.epoch = ++ctx->epoch;
         }
-    } else if (dt != SLAT_F64 && kNarrowCsr) {
+    } else if (dt != SLAT_F64 && kNarrowCsr && !tiny) {
         // B walked in CSR form: k_bvmax gives the numeric pass the same max(B) (narrow slots, and
         // hub rows accumulate in C instead of one re-traversal per rank chunk)
         a.b_vmax = ctx->d_vmax;
@@ -885,6 +903,23 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     } while (0)
 
     hc.mark(4);
+    hipError_t e;
+    const bool run_tiny = tiny && !exact;
+    if (run_tiny) {
+        // the whole call in one kernel: a wave per row, every block resident (<= 1024 blocks of
+        // <= 30 KB LDS), block offsets by look-back; it stores the completion word itself
+        a.c_col = C->col_idx;
+        a.c_val = C->values;
+        a.seq = ++ctx->done_seq;
+        a.done = ctx->d_words + 6;
+        const uint64_t g = row_blocks;
+        if ((st = ensure_status(ctx, g, s))) return failc(st);
+        const uint32_t epoch = slat_next_scan_epoch(ctx, s);
+        SLAT_HIPC(slat_launch_tiny(sem, dim3((unsigned)g), num_lds, s, a, ctx->d_status, epoch, ctx->d_words + 2));
+        hc.mark(5);
+        hc.mark(6);
+        SLAT_HIPC(wait_stream(ctx, s, a.seq));
+    } else {
     if (a.stats || SLAT_PHASES) SLAT_HIPC(hipMemsetAsync(a.shards, 0, shards_b, s));
     asym.counts = a.counts;
     asym.shards = a.shards;
@@ -898,7 +933,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     asym.nblk = a.nblk;
     asym.wsplit = a.wsplit;
     asym.wnch1 = a.wnch1;
-    hipError_t e;
     slat::FatArgs fat_args = {};
     slat::FatArgs *fa = &fat_args;
     if (fat) {
@@ -1009,6 +1043,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                                              hipMemcpyDeviceToHost, s));
     hc.mark(6);
     SLAT_HIPC(wait_stream(ctx, s, a.seq));
+    }  // regular pipeline
 #undef SLAT_HIPC
     hc.mark(7);
     if (SLAT_PHASES) {
@@ -1079,7 +1114,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     S.nnz = nnz;
     S.flops = flops;
     S.capacity = C->capacity;
-    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u);
+    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;

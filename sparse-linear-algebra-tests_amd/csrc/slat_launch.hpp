@@ -50,5 +50,9 @@ static inline int slat_numeric_blocks_per_cu(int sem, int mode, bool idx32, bool
 // symbolic: mode 0 every row by windows, 1 one row per hash table, 2 the listed / window rows
 hipError_t slat_launch_symbolic(int mode, bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s,
                                 const slat::Args &a);
+// the whole product of a small call in one kernel (slat_tiny.hip): status / epoch: the look-back
+// words of the blocks' offsets (as k_scan_rows'), maxw: the epoch-tagged max-row word
+hipError_t slat_launch_tiny(int sem, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a,
+                            unsigned long long *status, uint32_t epoch, unsigned long long *maxw);
 // the batched short-row symbolic of wide launches (lists the other rows for mode 2)
 hipError_t slat_launch_symbolic_short(bool idx32, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);

@@ -51,6 +51,12 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_PHASES
 #define SLAT_PHASES 0  // diagnostic builds: per-phase s_memtime cycles of k_numeric
 #endif
+#ifndef SLAT_SHORT_PACK
+#define SLAT_SHORT_PACK 1  // k_numeric_short: payload-free emit sort of (key << 9 | slot) when it fits 32 bits
+#endif
+#ifndef SLAT_SYM_CAP_PCT
+#define SLAT_SYM_CAP_PCT 70  // k_symbolic_short: a batch's product bound, % of the table's slots
+#endif
 #ifndef SLAT_AEARLY
 #define SLAT_AEARLY 1  // k_numeric: a long row's A values for the narrow bound loaded with its stored bitmap
 #endif
@@ -1996,7 +2002,7 @@ __host__ __device__ constexpr uint32_t sym_short_bytes() { return kSymHashT * 4 
 template <typename I>
 __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
     constexpr int kWpb = kBlock / kWave;
-    constexpr uint32_t kCap = kSymHashT * 7 / 10;
+    constexpr uint32_t kCap = kSymHashT * SLAT_SYM_CAP_PCT / 100;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -2219,7 +2225,9 @@ __host__ __device__ constexpr uint32_t short_bytes() {
 // (wave_sort256); a key's sorted position IS its output index in the batch, since keys are
 // composite (lr << cb | column, cb > 0) and the batch's rows are contiguous in C. The table is left
 // clean; zero values go to zero(local row).
-template <typename Sem, typename Z>
+// PACK: the batch's keys fit 23 bits (<= 8 local rows, cb <= 20), so key << 9 | slot is one u32 and the
+// sort moves no payload (half the lane exchanges and selects)
+template <typename Sem, bool PACK, typename Z>
 __device__ __forceinline__ void batch_emit(uint32_t *hkeys, typename Sem::V *hvals, uint32_t *hstage, uint32_t *hslot,
                                            uint32_t cb, uint32_t tot, uint32_t *oc, typename Sem::S *ov, Z &&zero) {
     using S = typename Sem::S;
@@ -2249,7 +2257,18 @@ __device__ __forceinline__ void batch_emit(uint32_t *hkeys, typename Sem::V *hva
     sfor<4>([&](auto E) {
         if (lane * 4 + E >= nk) k[E] = kSent;
     });
-    wave_sort256<true, uint32_t, true>(k, sl);  // distinct keys (kSent padding aside)
+    if constexpr (PACK) {
+        sfor<4>([&](auto E) {
+            if (k[E] != kSent) k[E] = (k[E] << 9) | sl[E];
+        });
+        wave_sort256<false, uint32_t, true>(k, sl);
+        sfor<4>([&](auto E) {
+            sl[E] = k[E] & (kHashT - 1);
+            if (k[E] != kSent) k[E] >>= 9;
+        });
+    } else {
+        wave_sort256<true, uint32_t, true>(k, sl);  // distinct keys (kSent padding aside)
+    }
     const uint32_t cmask = cb ? (1u << cb) - 1 : 0xFFFFFFFFu;
     sfor<4>([&](auto E) {
         const uint32_t i = lane * 4 + E;
@@ -2314,6 +2333,9 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
     S *cval = (S *)p.c_val;
     uint32_t zrows = 0;
     const uint32_t cb = p.cbits;
+    // packed emit keys (batch_emit PACK): batches of <= 8 rows whose composite keys, shifted past a
+    // 9-bit slot, stay below kSent
+    const bool pack = SLAT_SHORT_PACK && cb > 0 && cb <= 20 && ((((7ull << cb) | (p.ncols - 1)) << 9) | 511ull) < 0xFFFFFFFFull;
     const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
     PhaseClock pc{};  // diagnostic builds (SLAT_PHASES): where the waves' time goes
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
@@ -2346,7 +2368,8 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
             const uint32_t pu = wave_incl_scan(uu, 0u, [](uint32_t x, uint32_t y) { return x + y; });
             const uint32_t pl = wave_incl_scan(ll, 0u, [](uint32_t x, uint32_t y) { return x + y; });
             const unsigned long long stop = __ballot(inb && (!shortj || pu > kHashT / 2 || pl > 256 ||
-                                                             (cb == 0 && (uint32_t)lane > b)));
+                                                             (cb == 0 && (uint32_t)lane > b) ||
+                                                             (pack && (uint32_t)lane - b >= 8u)));
             const uint32_t e = stop ? (uint32_t)__builtin_ctzll(stop) : nt;
             pc.mark(0);  // tile header, batch formation
             pc.ph[kPhaseSlots - 1] += 1;
@@ -2427,8 +2450,11 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
             }
             wave_sync();
             pc.mark(2);  // ELL loads, hash accumulation
-            batch_emit<Sem>(hkeys, hvals, hstage, hslot, cb, lim, p.c_col + OB, cval + OB,
-                            [&](uint32_t lr) { atomicAdd(&zc[lr], 1u); });
+            auto zero = [&](uint32_t lr) { atomicAdd(&zc[lr], 1u); };
+            if (pack)
+                batch_emit<Sem, true>(hkeys, hvals, hstage, hslot, cb, lim, p.c_col + OB, cval + OB, zero);
+            else
+                batch_emit<Sem, false>(hkeys, hvals, hstage, hslot, cb, lim, p.c_col + OB, cval + OB, zero);
             pc.mark(3);  // emit
             if (inb && (uint32_t)lane < e) {
                 const uint32_t z = zc[lane - b];

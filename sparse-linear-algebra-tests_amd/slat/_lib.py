@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("SLAT_LIB_PATH") or os.path.join(PKG_DIR, "libslat.so"
 SLAT_OK, SLAT_EINVAL, SLAT_EDIM, SLAT_EOOM, SLAT_EHIP, SLAT_ENOTSUP, SLAT_ENODEV = range(7)
 U32, SAT64, F64 = 0, 1, 2
 DEVICE, HOST = 0, 1
-FLAG_TIMING, FLAG_EXACT_ALLOC, FLAG_STATS, FLAG_F64_ANY_ORDER, FLAG_IDX64 = 0x1, 0x2, 0x4, 0x8, 0x10
+FLAG_TIMING, FLAG_EXACT_ALLOC, FLAG_STATS, FLAG_F64_ANY_ORDER, FLAG_IDX64, FLAG_NO_TINY = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
 
 # Every symbol include/slat.h declares (checked by tests/test_abi.py).
 EXPORTS = [
