@@ -54,6 +54,34 @@ __host__ __device__ constexpr size_t fr_lds() {
 
 __device__ __forceinline__ uint32_t cap63(uint64_t x) { return x < 63 ? (uint32_t)x : 63u; }
 
+#ifndef SLAT_FAT_TICKET
+#define SLAT_FAT_TICKET 1
+#endif
+// The list's rows by block tickets instead of a fixed stride (power-law rows differ 40x in cost, so a
+// stride leaves blocks idle behind the ones that drew several hubs): block b starts on row b without a
+// ticket, each later row is a ticket (TicketQueue's protocol at block level: every block that had a
+// row takes exactly one ticket past the end, and the last taker zeroes the counter for the next
+// launch). Callers end each row with a block barrier.
+struct BlockTickets {
+    unsigned long long *ctr;
+    uint64_t total;
+    __device__ __forceinline__ BlockTickets(unsigned long long *c, uint64_t n)
+        : ctr(SLAT_FAT_TICKET ? c : nullptr),
+          total((n > gridDim.x ? n - gridDim.x : 0) + (n < gridDim.x ? n : (uint64_t)gridDim.x)) {}
+    __device__ __forceinline__ uint64_t next(uint64_t li, unsigned long long *sh) const {
+        if (!ctr) return li + gridDim.x;
+        if (threadIdx.x == 0) {
+            const unsigned long long t = atomicAdd(ctr, 1ull);
+            if (t == total - 1) __hip_atomic_store(ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *sh = t;
+        }
+        __syncthreads();
+        const uint64_t v = gridDim.x + *sh;
+        __syncthreads();
+        return v;
+    }
+};
+
 
 // products of each row, cut off at kFat; fat rows marked and listed
 __global__ __launch_bounds__(kBlock) void k_fr_select(FatArgs f) {
@@ -158,7 +186,28 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
                 const S at = readlane_val(a[Q], l0);
                 I s1 = s0, e1 = e0;
                 if (!all_cols) b_range<I>(p.b_col, s0, e0, lo, hi, s1, e1);
-                for (I j = s1 + (I)lane; j < e1; j += (I)kWave) fn(p.b_col[j], at, VALS ? bv[j] : S(0));
+                if constexpr (SLAT_LONG_UNROLL > 1) {
+                    // several 64-entry stretches per step: their loads in flight together
+                    constexpr int kLU = SLAT_LONG_UNROLL > 1 ? SLAT_LONG_UNROLL : 2;
+                    for (I j0 = s1 + (I)lane; j0 < e1; j0 += (I)(kLU * kWave)) {
+                        uint32_t cc[kLU];
+                        S vv[kLU];
+                        sfor<kLU>([&](auto U) {
+                            const I j = j0 + (I)(U * kWave);
+                            cc[U] = 0;
+                            vv[U] = S(0);
+                            if (j < e1) {
+                                cc[U] = p.b_col[j];
+                                if constexpr (VALS) vv[U] = bv[j];
+                            }
+                        });
+                        sfor<kLU>([&](auto U) {
+                            if (j0 + (I)(U * kWave) < e1) fn(cc[U], at, vv[U]);
+                        });
+                    }
+                } else {
+                    for (I j = s1 + (I)lane; j < e1; j += (I)kWave) fn(p.b_col[j], at, VALS ? bv[j] : S(0));
+                }
             }
         });
         mx = wave_max_u32(mx);
@@ -242,7 +291,9 @@ __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
     const unsigned int nl = *(volatile unsigned int *)f.cnt;
     for (uint32_t w = threadIdx.x; w < kWords; w += kFB) bits[w] = 0;
     __syncthreads();
-    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+    __shared__ unsigned long long s_tk;
+    const BlockTickets bt(f.tq, nl);
+    for (uint64_t li = blockIdx.x; li < nl; li = bt.next(li, &s_tk)) {
         const uint64_t row = f.list[li];
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         uint64_t count = 0;
@@ -471,7 +522,9 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
     const unsigned int nl = *(volatile unsigned int *)f.cnt;
     const uint32_t nbk = (uint32_t)((p.ncols + CH - 1) / CH);
     uint32_t zrows = 0;
-    for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+    __shared__ unsigned long long s_tk;
+    const BlockTickets bt(f.tq, nl);
+    for (uint64_t li = blockIdx.x; li < nl; li = bt.next(li, &s_tk)) {
         const uint64_t row = f.list[li];
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         const uint64_t ob = p.c_rp[row], oe = p.c_rp[row + 1];
@@ -567,6 +620,7 @@ slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
     f.bcol = nullptr;
     f.bval = nullptr;
     f.bcap = 0;
+    f.tq = ctx->d_words + 5;
     SLAT_HIP(ctx, hipMemsetAsync(f.cnt, 0, 4, s));
     a.fr_mark = f.mark;
     f.a = a;

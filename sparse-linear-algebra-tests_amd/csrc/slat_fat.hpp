@@ -25,6 +25,9 @@ struct FatArgs {
     uint32_t *bcol;
     void *bval;
     uint32_t bcap;
+    // row tickets (SLAT_FAT_TICKET; the context's ticket word, zero between launches): rows by a
+    // counter instead of a fixed stride over the blocks
+    unsigned long long *tq;
 };
 }  // namespace slat
 
