@@ -57,9 +57,6 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_LONG_UNROLL
 #define SLAT_LONG_UNROLL 4  // long B rows walked by the whole wave: 64-entry stretches per step (1, 4 or 8)
 #endif
-#ifndef SLAT_G8
-#define SLAT_G8 0  // RowWalker with the ELL copy: every entry's first two groups loaded at once, no tails
-#endif
 #ifndef SLAT_SYM_CAP_PCT
 #define SLAT_SYM_CAP_PCT 70  // k_symbolic_short: a batch's product bound, % of the table's slots
 #endif
@@ -1083,7 +1080,7 @@ struct RowWalker {
             if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
             if constexpr (Sem::kNarrowable) amax = max(amax, sat32(aq[Q]));
         });
-        if constexpr (!ELL || SLAT_G8) return;
+        if constexpr (!ELL) return;
         uint32_t mx = 0;
         sfor<kRegQ>([&](auto Q) {
             constexpr int q = Q;
@@ -1130,46 +1127,7 @@ struct RowWalker {
     // products are the one value prod(a, v0)
     template <bool VV, typename PSem = Sem, bool UNI = false, typename G>
     __device__ __forceinline__ void each_group(G &grp, S v0 = S(0)) {
-        if constexpr (ELL && SLAT_G8) {
-            // SLAT_G8: groups 0 and 1 of every entry (32 contiguous bytes of its ELL row) loaded at
-            // once, no group counts and no tail compaction; an entry whose group 1 is full walks its
-            // further groups alone (B rows of more than 8 entries)
-            const bool two = p.ell_wq > 1;  // launch-uniform
-            for (uint32_t sg = 0; sg < nseg; ++sg) {
-                if (!single) load_seg(a0 + (I)((uint64_t)sg * kSeg));
-                uint4 c0[kRegQ], c1[kRegQ];
-                Quad<S> p0[kRegQ], p1[kRegQ];
-                sfor<kRegQ>([&](auto Q) {
-                    constexpr int q = Q;
-                    c0[q] = c1[q] = make_uint4(kSent, kSent, kSent, kSent);
-                    p0[q] = p1[q] = Quad<S>{};
-                    if (kq[q] != kSent) {
-                        c0[q] = ell_cols(p, kq[q], 0);
-                        if (two) c1[q] = ell_cols(p, kq[q], 1);
-                        if constexpr (VV && !UNI) {
-                            p0[q] = ell_vals<S>(p, kq[q], 0);
-                            if (two) p1[q] = ell_vals<S>(p, kq[q], 1);
-                        }
-                    }
-                });
-                if constexpr (VV && UNI) {
-                    sfor<kRegQ>([&](auto Q) { p0[Q] = p1[Q] = splat4(PSem::prod(aq[Q], v0)); });
-                } else if constexpr (VV) {
-                    sfor<kRegQ>([&](auto Q) {
-                        p0[Q] = prods<PSem>(aq[Q], p0[Q]);
-                        p1[Q] = prods<PSem>(aq[Q], p1[Q]);
-                    });
-                }
-                grp.multi(c0, p0);
-                if (two) {
-                    grp.multi(c1, p1);
-                    if (p.ell_wq > 2)
-                        sfor<kRegQ>([&](auto Q) {
-                            if (kq[Q] != kSent && c1[Q].w != kSent) walk_brow<PSem, true, VV, I>(p, kq[Q], aq[Q], 2, grp);
-                        });
-                }
-            }
-        } else if constexpr (ELL) {
+        if constexpr (ELL) {
             for (uint32_t sg = 0; sg < nseg; ++sg) {
                 if (!single) load_seg(a0 + (I)((uint64_t)sg * kSeg));
                 if (nb == kOvf) {  // rare: too many tail items for the register batches
