@@ -37,7 +37,7 @@ namespace slat {
 
 constexpr int kFB = 512;                 // threads per fat-row block
 constexpr int kFW = kFB / kWave;         // waves per block
-constexpr uint64_t kFat = 16384;         // products per row from which a row is fat
+
 constexpr uint32_t kSymBits = 1u << 20;  // symbolic bitmap columns per pass (128 KB)
 
 // columns per accumulator chunk: 128 KB of V slots + the chunk's bitmap
@@ -83,7 +83,7 @@ struct BlockTickets {
 };
 
 
-// products of each row, cut off at kFat; fat rows marked and listed
+// products of each row, cut off at f.fat_min; fat rows marked and listed
 __global__ __launch_bounds__(kBlock) void k_fr_select(FatArgs f) {
     const Args &p = f.a;
     for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r - threadIdx.x < p.nrows;
@@ -91,11 +91,11 @@ __global__ __launch_bounds__(kBlock) void k_fr_select(FatArgs f) {
         bool fat = false;
         if (r < p.nrows) {
             uint64_t fl = 0;
-            for (uint64_t i = p.a_rp[r], e = p.a_rp[r + 1]; i < e && fl < kFat; ++i) {
+            for (uint64_t i = p.a_rp[r], e = p.a_rp[r + 1]; i < e && fl < f.fat_min; ++i) {
                 const uint32_t k = p.a_col[i];
                 if (k < p.b_nrows) fl += p.b_rp[k + 1] - p.b_rp[k];
             }
-            fat = fl >= kFat;
+            fat = fl >= f.fat_min;
             f.mark[r] = fat ? 1 : 0;
         }
         const unsigned long long m = __ballot(fat);
@@ -586,6 +586,15 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
 
 using namespace slat;
 
+// products per row from which a row is fat: 16384 (SLAT_FAT_MIN: A/B knob)
+uint64_t slat_fat_min() {
+    static const uint64_t v = [] {
+        const char *e = std::getenv("SLAT_FAT_MIN");
+        return e ? std::max<uint64_t>(256, std::strtoull(e, nullptr, 10)) : 16384ull;
+    }();
+    return v;
+}
+
 // workspace bytes of the fat-row category for n rows
 hipError_t slat_launch_splits(slat_ctx *ctx, const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb, uint32_t nch1,
                               uint32_t shift, uint32_t *split, hipStream_t s) {
@@ -621,6 +630,7 @@ slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
     f.bval = nullptr;
     f.bcap = 0;
     f.tq = ctx->d_words + 5;
+    f.fat_min = slat_fat_min();
     SLAT_HIP(ctx, hipMemsetAsync(f.cnt, 0, 4, s));
     a.fr_mark = f.mark;
     f.a = a;
@@ -703,8 +713,11 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
     h.bcol = nullptr;
     h.bval = nullptr;
     h.bcap = 0;
-    static const bool kNoBuckets = std::getenv("SLAT_NO_FAT_BUCKETS") != nullptr;  // A/B knob
-    if (!Sem::kOrdered && !kNoBuckets && (h.a.ncols + fr_chunk<Sem>() - 1) / fr_chunk<Sem>() <= kMaxBuckets) {
+    // (off by default: with the long B rows' loads in flight together, the per-chunk walks over B split
+    // by chunk beat the bucket scatter, which moves 4x the bytes: R-MAT 2^16 A^2 fat rows 7.4 GB /
+    // 6.9 ms against 1.8 GB / 3.6 ms, profiles/r03_fat_bucket_vs_rewalk.txt; SLAT_FAT_BUCKETS=1: on)
+    static const bool kBuckets = std::getenv("SLAT_FAT_BUCKETS") != nullptr;  // A/B knob
+    if (!Sem::kOrdered && kBuckets && (h.a.ncols + fr_chunk<Sem>() - 1) / fr_chunk<Sem>() <= kMaxBuckets) {
         const uint32_t cap = 1u << 19;
         const size_t nbk = (size_t)g.x * cap;
         if (slat_dev_alloc(ctx, (void **)&bcol, nbk * 4, ctx->stream) == hipSuccess &&

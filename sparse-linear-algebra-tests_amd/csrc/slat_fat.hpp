@@ -28,6 +28,7 @@ struct FatArgs {
     // row tickets (SLAT_FAT_TICKET; the context's ticket word, zero between launches): rows by a
     // counter instead of a fixed stride over the blocks
     unsigned long long *tq;
+    uint64_t fat_min;  // products per row from which a row is fat (slat_fat_min())
 };
 }  // namespace slat
 
@@ -35,6 +36,8 @@ struct FatArgs {
 // in B row k of its first column >= g << shift, g in [0, nch1) (the last = the row's length)
 hipError_t slat_launch_splits(slat_ctx *ctx, const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb, uint32_t nch1,
                               uint32_t shift, uint32_t *split, hipStream_t s);
+// products per row from which a row takes the fat-row kernels (16384; SLAT_FAT_MIN overrides)
+uint64_t slat_fat_min();
 // workspace bytes of the category for n rows
 size_t slat_fat_ws(uint64_t n);
 // mark and list the rows of >= 16384 products (sets a.fr_mark); nothing comes back to the host

@@ -124,3 +124,29 @@ def test_zeros_and_cancellation_in_fat_rows():
     fs = O.from_arrays(frp, fcol, fval, O.F64)
     fp = O.matmul_seq(fs, fs)
     assert_same(to_dev(fp, slat.CsrF64)._spgemm(to_dev(fs, slat.CsrF64)), O.matmul_seq(fp, fs), "f64 signs")
+
+
+def test_bucketed_products_knob():
+    """MAGNUS's fine-level reordering (the fat rows' products scattered by accumulator chunk into HBM,
+    then each chunk accumulated from its bucket) is off by default since round 3 (the per-chunk walks
+    over B split by chunk measured faster); SLAT_FAT_BUCKETS=1 turns it on. The
+    knob is read once per process, so the bucketed path runs in a child process here, against the
+    oracle, on the wide fat rows (3M columns, many chunks per row) and the zeros / cancellation case."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = """
+import sys
+sys.path[:0] = [{pkg!r}, {orc!r}, {tests!r}]
+import oracle_py as O
+import test_fat_rows_gpu as T
+for dt in (O.U32, O.F64):  # 3M columns: fat rows spanning many accumulator chunks take the buckets
+    T.test_wide_fat_rows_past_2_20_columns(dt)
+T.test_zeros_and_cancellation_in_fat_rows()
+print("ok")
+""".format(pkg=os.path.join(root, "sparse-linear-algebra-tests_amd"), orc=os.path.join(root, "oracle"),
+           tests=os.path.join(root, "tests"))
+    env = dict(os.environ, SLAT_FAT_BUCKETS="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
