@@ -692,7 +692,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                       !(flags & (SLAT_FLAG_TIMING | SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) &&
                       g_progress.load(std::memory_order_relaxed) == 0 &&
                       (unsigned __int128)a_nnz_block * maxrow_b <= (1u << 18) &&
-                      (A->max_row_nnz ? (unsigned __int128)A->max_row_nnz * maxrow_b < 16384 : maxrow_b <= 32);
+                      (A->max_row_nnz ? (unsigned __int128)A->max_row_nnz * maxrow_b < slat_fat_min() : maxrow_b <= 32);
     static const bool kNoEll = std::getenv("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
@@ -776,7 +776,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // batched wide launches: symbolic / numeric window-row lists u32[n] | their counters
     const size_t list_b = sym_batched ? up256(n * 4) : 0;
     const size_t o_l1 = o_smask + smask_b, o_l2 = o_l1 + list_b, o_lc = o_l2 + list_b, lc_b = sym_batched ? 256 : 0;
-    // fat rows (MAGNUS's dense-accumulation category) once a row can reach kFat products:
+    // fat rows (MAGNUS's dense-accumulation category) once a row can reach slat_fat_min() products:
     // max row of A x max row of B (A's max row unknown: when B has long rows)
     static const bool kNoFat = std::getenv("SLAT_NO_FAT") != nullptr;
     const uint64_t maxrow_a = A->max_row_nnz;

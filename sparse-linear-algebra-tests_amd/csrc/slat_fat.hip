@@ -6,7 +6,7 @@
 // re-walk of the row. Here such rows get a workgroup of 512 threads and the whole 160 KB LDS:
 //
 //   k_fr_select   one thread per row: products = sum over the row's entries k of nnz(B row k),
-//                 cut off at kFat; rows at or above it are marked (the other kernels skip them)
+//                 cut off at slat_fat_min(); rows at or above it are marked (the other kernels skip them)
 //                 and listed.
 //   k_fr_symbolic one block per listed row: a column bitmap over 2^20 columns per pass (128 KB),
 //                 one bit per product, popcount -> the row's structural count; also the mask of
@@ -586,11 +586,13 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
 
 using namespace slat;
 
-// products per row from which a row is fat: 16384 (SLAT_FAT_MIN: A/B knob)
+// products per row from which a row is fat: 8192 (16384 until round 3: rows between went to the window
+// pass's global-atomic hub path; 8192 measured R-MAT 2^16 A^2 numeric 8.67 -> 8.17 ms, C5 2^16 fold
+// 15.8 -> 13.7 ms, 2^18 fold 121 -> 114 ms, profiles/r03_ab_fat_min.txt; SLAT_FAT_MIN: A/B knob)
 uint64_t slat_fat_min() {
     static const uint64_t v = [] {
         const char *e = std::getenv("SLAT_FAT_MIN");
-        return e ? std::max<uint64_t>(256, std::strtoull(e, nullptr, 10)) : 16384ull;
+        return e ? std::max<uint64_t>(256, std::strtoull(e, nullptr, 10)) : 8192ull;
     }();
     return v;
 }
