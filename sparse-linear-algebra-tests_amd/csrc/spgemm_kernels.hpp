@@ -57,6 +57,9 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_LONG_UNROLL
 #define SLAT_LONG_UNROLL 4  // long B rows walked by the whole wave: 64-entry stretches per step (1, 4 or 8)
 #endif
+#ifndef SLAT_TAIL_BATCH
+#define SLAT_TAIL_BATCH 0  // RowWalker tail compaction: a round's permutes issued together
+#endif
 #ifndef SLAT_SYM_CAP_PCT
 #define SLAT_SYM_CAP_PCT 70  // k_symbolic_short: a batch's product bound, % of the table's slots
 #endif
@@ -779,7 +782,9 @@ __device__ __forceinline__ uint32_t hash_slot(uint32_t c, uint32_t logt) { retur
 // slots of N columns at once (kSent = no column): every probe round issues all pending CAS
 // before it looks at any result, so the LDS latency is paid once per round, not once per column.
 // fresh[i]: this call inserted column i.
-template <int N>
+// NB: the first round branch-free (below); the numeric tables take it, symbolic's do not (C4: numeric
+// 0.825 -> 0.806 ms, symbolic 0.411 -> 0.432 ms with it, profiles/r03_ab_nb2_ballot.txt)
+template <int N, bool NB = false>
 __device__ __forceinline__ void hash_batch(uint32_t *keys, uint32_t logt, const uint32_t (&c)[N], uint32_t (&sl)[N],
                                            bool (&fresh)[N]) {
     const uint32_t mask = (1u << logt) - 1;
@@ -789,6 +794,30 @@ __device__ __forceinline__ void hash_batch(uint32_t *keys, uint32_t logt, const 
         sl[i] = hash_slot(c[i], logt);
         fresh[i] = false;
         if (c[i] != kSent) pend |= 1u << i;
+    }
+    if constexpr (NB) {
+        // The first round branch-free: every key issues its CAS, a padding key on the lane's own
+        // dummy word (zero, never kSent: the CAS fails and writes nothing; one word per lane, so no
+        // two lanes of an instruction share an address), so the round's CASes issue back to back.
+        // With a branch per key the compiler cannot prove a skipped key's last CAS result has landed
+        // and waits for all LDS traffic (lgkmcnt(0)) before every CAS. Later rounds, with few keys
+        // left, keep the branches (a key no lane needs issues nothing).
+        __shared__ uint32_t s_dummy[kWave];
+        const uint32_t lane = (uint32_t)lane_id();
+        s_dummy[lane] = 0;
+        uint32_t prev[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) prev[i] = atomicCAS((pend >> i) & 1u ? &keys[sl[i]] : &s_dummy[lane], kSent, c[i]);
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            if ((pend >> i) & 1u) {
+                if (prev[i] == kSent || prev[i] == c[i]) {
+                    fresh[i] = prev[i] == kSent;
+                    pend &= ~(1u << i);
+                } else {
+                    sl[i] = (sl[i] + 1) & mask;
+                }
+            }
     }
     while (__builtin_amdgcn_readfirstlane(__ballot(pend != 0) != 0)) {
         uint32_t prev[N];
@@ -855,7 +884,7 @@ struct HashAcc {
             cc[4 * q + 2] = c[q].z;
             cc[4 * q + 3] = c[q].w;
         }
-        hash_batch<4 * Q>(keys, 9, cc, sl, fresh);  // kHashT = 2^9
+        hash_batch<4 * Q, true>(keys, 9, cc, sl, fresh);  // kHashT = 2^9
 #pragma unroll
         for (int i = 0; i < 4 * Q; ++i)
             if (cc[i] != kSent) Sem::acc(vals, sl[i], pr[i / 4].v[i % 4]);
@@ -863,7 +892,7 @@ struct HashAcc {
     __device__ __forceinline__ void put(uint32_t c, S pr) {
         uint32_t cc[1] = {c}, sl[1];
         bool fresh[1];
-        hash_batch<1>(keys, 9, cc, sl, fresh);
+        hash_batch<1, true>(keys, 9, cc, sl, fresh);
         if (c != kSent) Sem::acc(vals, sl[0], pr);
     }
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) { run<1>(&c, &pr); }
@@ -1090,6 +1119,49 @@ struct RowWalker {
         mx = wave_max_u32(mx);
         bk0 = bk1 = kSent;
         uint32_t off = 0;  // items placed so far (uniform)
+        if constexpr (SLAT_TAIL_BATCH) {
+            // every round's destinations first (they depend on ballots only), then all its
+            // permutes, then the selects: one LDS round trip per round instead of one per q (the
+            // compiler waited on each q's permute before issuing the next q's)
+            for (uint32_t t = 1; t < mx; ++t) {
+                int dst[kRegQ];
+                uint32_t oq[kRegQ], cq[kRegQ];
+                sfor<kRegQ>([&](auto Q) {
+                    constexpr int q = Q;
+                    const bool has = ngq[q] > t;
+                    const unsigned long long m = __ballot(has);
+                    const uint32_t cnt = __popcll(m);
+                    const uint32_t below =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    dst[q] = (int)(((has ? off + below : off + cnt) & (kWave - 1)) * 4);
+                    oq[q] = off;
+                    cq[q] = cnt;
+                    off += cnt;
+                });
+                uint32_t rk[kRegQ];
+                S ra[kRegQ];
+                sfor<kRegQ>([&](auto Q) {
+                    rk[Q] = (uint32_t)__builtin_amdgcn_ds_permute(dst[Q], (int)kq[Q]);
+                    ra[Q] = AVALS ? permute_val(dst[Q], aq[Q]) : S(0);
+                });
+                sfor<kRegQ>([&](auto Q) {
+                    constexpr int q = Q;
+                    const uint32_t i = ((uint32_t)lane - oq[q]) & (kWave - 1);  // receive slot
+                    const uint32_t g = oq[q] + i;                               // item index -> batch g / 64
+                    const bool in0 = (i < cq[q]) & (g < (uint32_t)kWave);
+                    const bool in1 = (i < cq[q]) & (g >= (uint32_t)kWave) & (g < 2u * kWave);
+                    bk0 = in0 ? rk[q] : bk0;
+                    ba0 = in0 ? ra[q] : ba0;
+                    bt0 = in0 ? t : bt0;
+                    bk1 = in1 ? rk[q] : bk1;
+                    ba1 = in1 ? ra[q] : ba1;
+                    bt1 = in1 ? t : bt1;
+                });
+            }
+            nb = (off + kWave - 1) / kWave;
+            if (nb > kNB) nb = kOvf;
+            return;
+        }
         for (uint32_t t = 1; t < mx; ++t) {
             sfor<kRegQ>([&](auto Q) {
                 constexpr int q = Q;
@@ -1411,8 +1483,8 @@ __device__ __forceinline__ uint64_t sym_row(const Args &p, uint64_t row, bool li
             // count = popcount of the touched 64-word blocks only (word b*64 + lane per lane),
             // which the same lanes then clear
             uint32_t lc = 0;
-            const uint32_t bmask = wave_or_u32(sp.bm.blk);
             uint32_t *keep = nullptr;  // the stored bitmap of this row (Z launches with p.sbm)
+            const uint32_t bmask = wave_or_u32(sp.bm.blk);
             if constexpr (Z)
                 if (p.sbm) {
                     keep = p.sbm + row * ((uint64_t)p.nblk * kWave);

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-3 call ab: the GPU suite, smoke and the default bench line on the tree (numeric hash tables'
+# first probe round branch-free); C4 kernel trace
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/r03ab; mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+tail -n 1 $OUT/pytest.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+cat $OUT/smoke.log
+timeout -k 10 240 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/c4 -o c4 --output-format csv -- python3 tools/prof_c4.py > $OUT/c4.log 2>&1 || { tail -20 $OUT/c4.log; exit 1; }
+grep "^C4" $OUT/c4.log | tail -3
+echo done
