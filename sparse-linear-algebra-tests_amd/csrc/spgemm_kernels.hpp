@@ -57,8 +57,14 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_LONG_UNROLL
 #define SLAT_LONG_UNROLL 4  // long B rows walked by the whole wave: 64-entry stretches per step (1, 4 or 8)
 #endif
-#ifndef SLAT_TAIL_BATCH
-#define SLAT_TAIL_BATCH 0  // RowWalker tail compaction: a round's permutes issued together
+#ifndef SLAT_EMIT_UNROLL
+#define SLAT_EMIT_UNROLL 0  // k_numeric's emit: four 64-slot stretches per step
+#endif
+#ifndef SLAT_SYM_POPC8
+#define SLAT_SYM_POPC8 0  // symbolic: up to eight touched blocks' popcounts per step
+#endif
+#ifndef SLAT_ACC_Q
+#define SLAT_ACC_Q 1  // k_numeric's accumulate: groups per batch of rank lookups (1, 2 or 4)
 #endif
 #ifndef SLAT_SYM_CAP_PCT
 #define SLAT_SYM_CAP_PCT 70  // k_symbolic_short: a batch's product bound, % of the table's slots
@@ -1119,49 +1125,6 @@ struct RowWalker {
         mx = wave_max_u32(mx);
         bk0 = bk1 = kSent;
         uint32_t off = 0;  // items placed so far (uniform)
-        if constexpr (SLAT_TAIL_BATCH) {
-            // every round's destinations first (they depend on ballots only), then all its
-            // permutes, then the selects: one LDS round trip per round instead of one per q (the
-            // compiler waited on each q's permute before issuing the next q's)
-            for (uint32_t t = 1; t < mx; ++t) {
-                int dst[kRegQ];
-                uint32_t oq[kRegQ], cq[kRegQ];
-                sfor<kRegQ>([&](auto Q) {
-                    constexpr int q = Q;
-                    const bool has = ngq[q] > t;
-                    const unsigned long long m = __ballot(has);
-                    const uint32_t cnt = __popcll(m);
-                    const uint32_t below =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    dst[q] = (int)(((has ? off + below : off + cnt) & (kWave - 1)) * 4);
-                    oq[q] = off;
-                    cq[q] = cnt;
-                    off += cnt;
-                });
-                uint32_t rk[kRegQ];
-                S ra[kRegQ];
-                sfor<kRegQ>([&](auto Q) {
-                    rk[Q] = (uint32_t)__builtin_amdgcn_ds_permute(dst[Q], (int)kq[Q]);
-                    ra[Q] = AVALS ? permute_val(dst[Q], aq[Q]) : S(0);
-                });
-                sfor<kRegQ>([&](auto Q) {
-                    constexpr int q = Q;
-                    const uint32_t i = ((uint32_t)lane - oq[q]) & (kWave - 1);  // receive slot
-                    const uint32_t g = oq[q] + i;                               // item index -> batch g / 64
-                    const bool in0 = (i < cq[q]) & (g < (uint32_t)kWave);
-                    const bool in1 = (i < cq[q]) & (g >= (uint32_t)kWave) & (g < 2u * kWave);
-                    bk0 = in0 ? rk[q] : bk0;
-                    ba0 = in0 ? ra[q] : ba0;
-                    bt0 = in0 ? t : bt0;
-                    bk1 = in1 ? rk[q] : bk1;
-                    ba1 = in1 ? ra[q] : ba1;
-                    bt1 = in1 ? t : bt1;
-                });
-            }
-            nb = (off + kWave - 1) / kWave;
-            if (nb > kNB) nb = kOvf;
-            return;
-        }
         for (uint32_t t = 1; t < mx; ++t) {
             sfor<kRegQ>([&](auto Q) {
                 constexpr int q = Q;
@@ -1373,8 +1336,11 @@ struct AccPass {
         if constexpr (SLAT_PHASES) pc->mark(11);  // atomics issued
     }
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) { run<1>(&c, &pr); }
+    // SLAT_ACC_Q groups' rank lookups issued before any is used (one LDS round trip per SLAT_ACC_Q
+    // groups instead of per group)
     __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
-        sfor<kRegQ>([&](auto Q) { run<1>(c + Q, pr + Q); });
+        static_assert(kRegQ % SLAT_ACC_Q == 0, "SLAT_ACC_Q divides kRegQ");
+        sfor<kRegQ / SLAT_ACC_Q>([&](auto Q) { run<SLAT_ACC_Q>(c + Q * SLAT_ACC_Q, pr + Q * SLAT_ACC_Q); });
     }
 };
 
@@ -1490,12 +1456,32 @@ __device__ __forceinline__ uint64_t sym_row(const Args &p, uint64_t row, bool li
                     keep = p.sbm + row * ((uint64_t)p.nblk * kWave);
                     if (lane == 0) p.smask[row] = bmask;
                 }
-            for (uint32_t m = bmask; m; m &= m - 1) {
-                const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
-                const uint32_t x = L0[w];
-                lc += __popc(x);
-                L0[w] = 0;
-                if (keep) keep[w] = x;
+            if constexpr (SLAT_SYM_POPC8) {
+                // up to eight touched blocks per step: their LDS reads issued together (one LDS
+                // round trip per step instead of one per block)
+                for (uint32_t m = bmask; m;) {
+                    uint32_t ws[8], xs[8];
+                    sfor<8>([&](auto I_) {
+                        ws[I_] = m ? (uint32_t)__builtin_ctz(m) * kWave + lane : 0xFFFFFFFFu;
+                        m &= m - 1;
+                    });
+                    sfor<8>([&](auto I_) { xs[I_] = ws[I_] != 0xFFFFFFFFu ? L0[ws[I_]] : 0u; });
+                    sfor<8>([&](auto I_) {
+                        if (ws[I_] != 0xFFFFFFFFu) {
+                            lc += __popc(xs[I_]);
+                            L0[ws[I_]] = 0;
+                            if (keep) keep[ws[I_]] = xs[I_];
+                        }
+                    });
+                }
+            } else {
+                for (uint32_t m = bmask; m; m &= m - 1) {
+                    const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
+                    const uint32_t x = L0[w];
+                    lc += __popc(x);
+                    L0[w] = 0;
+                    if (keep) keep[w] = x;
+                }
             }
             cnt += wave_sum_u32(lc);
             if (first && p.stats) flops += wave_sum_u32(sp.nprod);
@@ -1874,6 +1860,43 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
                     uint32_t *oc = p.c_col + out_pos;
                     S *ov = cval + out_pos;
                     const uint32_t lim = (uint32_t)min<uint64_t>(out_end - min(out_pos, out_end), nch);
+                    if constexpr (SLAT_EMIT_UNROLL) {
+                        // four 64-slot stretches per step: their LDS reads issued together (the
+                        // loop below waits out one LDS round trip per 64 slots)
+                        for (uint32_t t0 = lane; t0 < nch; t0 += 4 * kWave) {
+                            S v[4];
+                            uint32_t cl[4];
+                            sfor<4>([&](auto U) {
+                                const uint32_t t = t0 + U * kWave;
+                                v[U] = S(0);
+                                cl[U] = 0;
+                                if (t < nch) {
+                                    if constexpr (NW)
+                                        v[U] = (S)vals[t];
+                                    else
+                                        v[U] = Sem::finish((const V *)vals, t);
+                                    cl[U] = cols[t];
+                                }
+                            });
+                            sfor<4>([&](auto U) {
+                                const uint32_t t = t0 + U * kWave;
+                                if (t < nch) {
+#pragma unroll
+                                    for (uint32_t w = 0; w < kVW; ++w) vals[t * kVW + w] = VS(0);
+                                    cols[t] = 0;
+                                    zeros += Sem::is_zero(v[U]) ? 1u : 0u;
+                                    if (t < lim && !(p.ablate & 16u)) {
+                                        oc[t] = wlo + cl[U];
+                                        ov[t] = v[U];
+                                    }
+                                }
+                            });
+                        }
+                        out_pos += nch;
+                        wave_sync();
+                        mark(4);
+                        return;
+                    }
                     for (uint32_t t = lane; t < nch; t += kWave) {
                         S v;
                         if constexpr (NW)
