@@ -57,14 +57,8 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_LONG_UNROLL
 #define SLAT_LONG_UNROLL 4  // long B rows walked by the whole wave: 64-entry stretches per step (1, 4 or 8)
 #endif
-#ifndef SLAT_EMIT_UNROLL
-#define SLAT_EMIT_UNROLL 0  // k_numeric's emit: four 64-slot stretches per step
-#endif
-#ifndef SLAT_SYM_POPC8
-#define SLAT_SYM_POPC8 0  // symbolic: up to eight touched blocks' popcounts per step
-#endif
 #ifndef SLAT_ACC_Q
-#define SLAT_ACC_Q 1  // k_numeric's accumulate: groups per batch of rank lookups (1, 2 or 4)
+#define SLAT_ACC_Q 4  // k_numeric's accumulate, 32-bit values: groups per batch of rank lookups (1, 2 or 4)
 #endif
 #ifndef SLAT_SYM_CAP_PCT
 #define SLAT_SYM_CAP_PCT 70  // k_symbolic_short: a batch's product bound, % of the table's slots
@@ -1336,11 +1330,13 @@ struct AccPass {
         if constexpr (SLAT_PHASES) pc->mark(11);  // atomics issued
     }
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &pr) { run<1>(&c, &pr); }
-    // SLAT_ACC_Q groups' rank lookups issued before any is used (one LDS round trip per SLAT_ACC_Q
-    // groups instead of per group)
+    // several groups' rank lookups issued before any is used: one LDS round trip per kAccQ groups
+    // instead of per group. 4 for 32-bit values (headline numeric 89.7 -> 87.6 us), 2 for 64-bit ones
+    // (4 took the Sat64 instance 103 -> 141 us), profiles/r03_ab_eu_sp8_aq.txt
+    static constexpr int kAccQ = sizeof(S) == 4 ? SLAT_ACC_Q : 2;
     __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) {
-        static_assert(kRegQ % SLAT_ACC_Q == 0, "SLAT_ACC_Q divides kRegQ");
-        sfor<kRegQ / SLAT_ACC_Q>([&](auto Q) { run<SLAT_ACC_Q>(c + Q * SLAT_ACC_Q, pr + Q * SLAT_ACC_Q); });
+        static_assert(kRegQ % kAccQ == 0, "kAccQ divides kRegQ");
+        sfor<kRegQ / kAccQ>([&](auto Q) { run<kAccQ>(c + Q * kAccQ, pr + Q * kAccQ); });
     }
 };
 
@@ -1456,32 +1452,12 @@ __device__ __forceinline__ uint64_t sym_row(const Args &p, uint64_t row, bool li
                     keep = p.sbm + row * ((uint64_t)p.nblk * kWave);
                     if (lane == 0) p.smask[row] = bmask;
                 }
-            if constexpr (SLAT_SYM_POPC8) {
-                // up to eight touched blocks per step: their LDS reads issued together (one LDS
-                // round trip per step instead of one per block)
-                for (uint32_t m = bmask; m;) {
-                    uint32_t ws[8], xs[8];
-                    sfor<8>([&](auto I_) {
-                        ws[I_] = m ? (uint32_t)__builtin_ctz(m) * kWave + lane : 0xFFFFFFFFu;
-                        m &= m - 1;
-                    });
-                    sfor<8>([&](auto I_) { xs[I_] = ws[I_] != 0xFFFFFFFFu ? L0[ws[I_]] : 0u; });
-                    sfor<8>([&](auto I_) {
-                        if (ws[I_] != 0xFFFFFFFFu) {
-                            lc += __popc(xs[I_]);
-                            L0[ws[I_]] = 0;
-                            if (keep) keep[ws[I_]] = xs[I_];
-                        }
-                    });
-                }
-            } else {
-                for (uint32_t m = bmask; m; m &= m - 1) {
-                    const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
-                    const uint32_t x = L0[w];
-                    lc += __popc(x);
-                    L0[w] = 0;
-                    if (keep) keep[w] = x;
-                }
+            for (uint32_t m = bmask; m; m &= m - 1) {
+                const uint32_t w = (uint32_t)__builtin_ctz(m) * kWave + lane;
+                const uint32_t x = L0[w];
+                lc += __popc(x);
+                L0[w] = 0;
+                if (keep) keep[w] = x;
             }
             cnt += wave_sum_u32(lc);
             if (first && p.stats) flops += wave_sum_u32(sp.nprod);
@@ -1860,43 +1836,6 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
                     uint32_t *oc = p.c_col + out_pos;
                     S *ov = cval + out_pos;
                     const uint32_t lim = (uint32_t)min<uint64_t>(out_end - min(out_pos, out_end), nch);
-                    if constexpr (SLAT_EMIT_UNROLL) {
-                        // four 64-slot stretches per step: their LDS reads issued together (the
-                        // loop below waits out one LDS round trip per 64 slots)
-                        for (uint32_t t0 = lane; t0 < nch; t0 += 4 * kWave) {
-                            S v[4];
-                            uint32_t cl[4];
-                            sfor<4>([&](auto U) {
-                                const uint32_t t = t0 + U * kWave;
-                                v[U] = S(0);
-                                cl[U] = 0;
-                                if (t < nch) {
-                                    if constexpr (NW)
-                                        v[U] = (S)vals[t];
-                                    else
-                                        v[U] = Sem::finish((const V *)vals, t);
-                                    cl[U] = cols[t];
-                                }
-                            });
-                            sfor<4>([&](auto U) {
-                                const uint32_t t = t0 + U * kWave;
-                                if (t < nch) {
-#pragma unroll
-                                    for (uint32_t w = 0; w < kVW; ++w) vals[t * kVW + w] = VS(0);
-                                    cols[t] = 0;
-                                    zeros += Sem::is_zero(v[U]) ? 1u : 0u;
-                                    if (t < lim && !(p.ablate & 16u)) {
-                                        oc[t] = wlo + cl[U];
-                                        ov[t] = v[U];
-                                    }
-                                }
-                            });
-                        }
-                        out_pos += nch;
-                        wave_sync();
-                        mark(4);
-                        return;
-                    }
                     for (uint32_t t = lane; t < nch; t += kWave) {
                         S v;
                         if constexpr (NW)
