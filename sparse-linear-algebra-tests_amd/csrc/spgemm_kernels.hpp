@@ -60,6 +60,9 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_ACC_Q
 #define SLAT_ACC_Q 4  // k_numeric's accumulate, 32-bit values: groups per batch of rank lookups (1, 2 or 4)
 #endif
+#ifndef SLAT_MK_HOIST
+#define SLAT_MK_HOIST 1  // short-row batches: the entry -> row marker reads issued together
+#endif
 #ifndef SLAT_SYM_CAP_PCT
 #define SLAT_SYM_CAP_PCT 70  // k_symbolic_short: a batch's product bound, % of the table's slots
 #endif
@@ -2117,9 +2120,16 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
             if (inb && (uint32_t)lane < e && lj > 0) atomicMax(&marks[(uint32_t)(A0j - A0)], (uint32_t)lane - b + 1);
             wave_sync();
             uint32_t kq[kRegQ], lq[kRegQ], ng[kRegQ], carry = 0, mxg = 0;
+            // (SLAT_MK_HOIST: every round's marker read issued before the first scan)
+            uint32_t mks[kRegQ];
+            if constexpr (SLAT_MK_HOIST)
+                sfor<kRegQ>([&](auto Q) {
+                    const uint32_t i = Q * kWave + lane;
+                    mks[Q] = i < nent ? marks[i] : 0u;
+                });
             sfor<kRegQ>([&](auto Q) {
                 const uint32_t i = Q * kWave + lane;
-                const uint32_t mk = i < nent ? marks[i] : 0u;
+                const uint32_t mk = SLAT_MK_HOIST ? mks[Q] : (i < nent ? marks[i] : 0u);
                 const uint32_t run = max(wave_incl_scan(mk, 0u, [](uint32_t x, uint32_t y) { return max(x, y); }), carry);
                 carry = readlane_u32(run, kWave - 1);
                 lq[Q] = run - 1;
@@ -2155,8 +2165,9 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
                         cc[3] = c.w != kSent ? (hi | c.w) : kSent;
                     }
                     bool fresh[4];
+                    if (p.stats)  // launch-uniform: no VALU for the product count otherwise
 #pragma unroll
-                    for (int x = 0; x < 4; ++x) nprod += cc[x] != kSent ? 1u : 0u;
+                        for (int x = 0; x < 4; ++x) nprod += cc[x] != kSent ? 1u : 0u;
                     hash_batch<4>(keys, 10, cc, sl, fresh);
                     const uint32_t f = (uint32_t)fresh[0] + fresh[1] + fresh[2] + fresh[3];
                     if (f) atomicAdd(&rcnt[lr], f);
@@ -2445,9 +2456,16 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
             uint32_t kq[kRegQ], lq[kRegQ], ng[kRegQ];
             S aq[kRegQ];
             uint32_t carry = 0, mxg = 0;
+            // (SLAT_MK_HOIST: every round's marker read issued before the first scan)
+            uint32_t mks[kRegQ];
+            if constexpr (SLAT_MK_HOIST)
+                sfor<kRegQ>([&](auto Q) {
+                    const uint32_t i = Q * kWave + lane;
+                    mks[Q] = i < nent ? marks[i] : 0u;
+                });
             sfor<kRegQ>([&](auto Q) {
                 const uint32_t i = Q * kWave + lane;
-                const uint32_t mk = i < nent ? marks[i] : 0u;
+                const uint32_t mk = SLAT_MK_HOIST ? mks[Q] : (i < nent ? marks[i] : 0u);
                 const uint32_t run = max(wave_incl_scan(mk, 0u, [](uint32_t x, uint32_t y) { return max(x, y); }), carry);
                 carry = readlane_u32(run, kWave - 1);
                 lq[Q] = run - 1;
