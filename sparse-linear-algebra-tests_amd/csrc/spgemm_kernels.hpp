@@ -63,9 +63,6 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_MK_HOIST
 #define SLAT_MK_HOIST 1  // short-row batches: the entry -> row marker reads issued together
 #endif
-#ifndef SLAT_TAIL_LDS
-#define SLAT_TAIL_LDS 0  // numeric's stored-bitmap rows: tail items compacted through LDS, not ds_permute
-#endif
 #ifndef SLAT_SYM_CAP_PCT
 #define SLAT_SYM_CAP_PCT 70  // k_symbolic_short: a batch's product bound, % of the table's slots
 #endif
@@ -1077,18 +1074,11 @@ struct RowWalker {
     uint32_t amax = 0;  // lane max of the A values seen (narrow-slot bound, u32)
     uint32_t sg0 = 0, sg1 = 0;  // CSR B: walk only column chunks [sg0, sg1) of each B row (p.wsplit)
 
-    // stage (SLAT_TAIL_LDS; null = none): 256 words of LDS the walker may use as scratch while the
-    // constructor compacts a one-segment row's tail items (numeric's bitmap region before the stored
-    // bitmap is loaded into it)
-    __device__ __forceinline__ RowWalker(const Args &p_, I a0_, I a1_, uint32_t *stage = nullptr)
-        : p(p_), a0(a0_), a1(a1_) {
+    __device__ __forceinline__ RowWalker(const Args &p_, I a0_, I a1_) : p(p_), a0(a0_), a1(a1_) {
         len = (uint64_t)(a1 - a0);
         nseg = (uint32_t)((len + kSeg - 1) / kSeg);
         single = nseg == 1;
-        if (single) {
-            seg_loads(p, a0, a1, kq, aq);
-            finish_seg(stage);
-        }
+        if (single) load_seg(a0);
     }
     // the A entries [sb, min(a1, sb + kSeg)) of a row, kRegQ per lane (kSent / 0 past the end)
     __device__ static __forceinline__ void seg_loads(const Args &p, I sb, I a1, uint32_t *k, S *a) {
@@ -1116,7 +1106,7 @@ struct RowWalker {
     }
 
     // group counts and the compacted tail batches of the segment in kq / aq
-    __device__ __forceinline__ void finish_seg(uint32_t *stage = nullptr) {
+    __device__ __forceinline__ void finish_seg() {
         const int lane = lane_id();
         sfor<kRegQ>([&](auto Q) {
             if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
@@ -1132,43 +1122,6 @@ struct RowWalker {
         mx = wave_max_u32(mx);
         bk0 = bk1 = kSent;
         uint32_t off = 0;  // items placed so far (uniform)
-        if constexpr (SLAT_TAIL_LDS && sizeof(S) == 4) if (stage) {
-            // tail items scattered into LDS at their ballot rank (B row | group << 24: ELL B rows are
-            // < 2^24), then each lane reads its item of both batches back: ~8 VALU per (round, q)
-            // instead of the permute compaction's ~20
-            uint32_t *sk = stage, *sa = stage + 2 * kWave;
-            for (uint32_t t = 1; t < mx; ++t) {
-                sfor<kRegQ>([&](auto Q) {
-                    constexpr int q = Q;
-                    const bool has = ngq[q] > t;
-                    const unsigned long long m = __ballot(has);
-                    const uint32_t at =
-                        off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    if (has && at < 2u * kWave) {
-                        sk[at] = kq[q] | (t << 24);
-                        if constexpr (AVALS) sa[at] = __builtin_bit_cast(uint32_t, aq[q]);
-                    }
-                    off += (uint32_t)__popcll(m);
-                });
-            }
-            wave_sync();
-            if (lane < off) {
-                const uint32_t x = sk[lane];
-                bk0 = x & 0xFFFFFFu;
-                bt0 = x >> 24;
-                if constexpr (AVALS) ba0 = __builtin_bit_cast(S, sa[lane]);
-            }
-            if (lane + kWave < off) {
-                const uint32_t x = sk[kWave + lane];
-                bk1 = x & 0xFFFFFFu;
-                bt1 = x >> 24;
-                if constexpr (AVALS) ba1 = __builtin_bit_cast(S, sa[kWave + lane]);
-            }
-            wave_sync();
-            nb = (off + kWave - 1) / kWave;
-            if (nb > kNB) nb = kOvf;
-            return;
-        }
         for (uint32_t t = 1; t < mx; ++t) {
             sfor<kRegQ>([&](auto Q) {
                 constexpr int q = Q;
@@ -1739,8 +1692,7 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
             wave_sync();
             }
         } else if (a1 > a0) {
-            // (SLAT_TAIL_LDS: the bitmap region is scratch until the stored bitmap is loaded)
-            RW rw(p, a0, a1, (SLAT_TAIL_LDS && MODE == 0 && !p.wide && p.sbm && p.ww >= 128) ? L0 : nullptr);
+            RW rw(p, a0, a1);
             const uint64_t len = rw.len;
             if constexpr (SLAT_PHASES) pin(rw.kq[0]);  // wait for the A entries inside phase 0
             mark(0);  // row bounds + A entries, group counts, tail compaction
