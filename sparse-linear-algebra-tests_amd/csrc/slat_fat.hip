@@ -40,10 +40,21 @@ constexpr int kFW = kFB / kWave;         // waves per block
 
 constexpr uint32_t kSymBits = 1u << 20;  // symbolic bitmap columns per pass (128 KB)
 
-// columns per accumulator chunk: 128 KB of V slots + the chunk's bitmap
+// columns per accumulator chunk: fr_kb<Sem>() KB of V slots + the chunk's bitmap. 64 KB (two blocks
+// per CU, twice the chunks per row) for the semirings that add with atomics: R-MAT 2^16 A^2
+// 11.7 -> 10.6 ms, C5 2^18 any order 92.5 -> 81.5 ms; 128 KB (one block per CU) for f64 in the
+// reference's fold order, whose wave slices halve with the chunk (C5 2^18 fold 110 -> 256 ms at 64 KB),
+// profiles/r03_ab_fr64.txt. SLAT_FR_KB overrides the 64.
+#ifndef SLAT_FR_KB
+#define SLAT_FR_KB 64
+#endif
+template <typename Sem>
+__host__ __device__ constexpr uint32_t fr_kb() {
+    return Sem::kOrdered ? 128u : (uint32_t)SLAT_FR_KB;
+}
 template <typename Sem>
 __host__ __device__ constexpr uint32_t fr_chunk() {
-    return (128u * 1024u) / (uint32_t)(sizeof(typename Sem::V) * Sem::kSlots);
+    return (fr_kb<Sem>() * 1024u) / (uint32_t)(sizeof(typename Sem::V) * Sem::kSlots);
 }
 constexpr uint32_t kMaxBuckets = 256;  // accumulator chunks a bucketed row may span (LDS counters)
 template <typename Sem>
@@ -669,7 +680,7 @@ static const uint64_t kSplitBytes = [] {
 
 template <typename Sem>
 static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
-    const dim3 g((unsigned)ctx->cu_count);
+    const dim3 g((unsigned)ctx->cu_count * (128u / fr_kb<Sem>()));  // the resident blocks
     const size_t lds = fr_lds<Sem>();
     // the chunk mask's granule must be a multiple of this instance's chunk
     FatArgs h = f;

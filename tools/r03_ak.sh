@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-3 call ak: the GPU suite on the tree (fat rows: 64 KB chunks for the atomic semirings), the
+# heavy products, the default bench line
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/r03ak; mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+tail -n 1 $OUT/pytest.log
+timeout -k 10 900 python tools/ab_heavy.py --reps 2 --big tree > $OUT/ab_heavy.txt 2>&1 || { tail -30 $OUT/ab_heavy.txt; exit 1; }
+grep -A2 summary $OUT/ab_heavy.txt
+timeout -k 10 240 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+echo done
