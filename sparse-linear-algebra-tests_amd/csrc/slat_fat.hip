@@ -294,7 +294,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sh, ui
 template <typename I>
 __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
     const Args &p = f.a;
-    constexpr uint32_t kWords = kSymBits / 32;
+    // the pass width: f.sym_bits columns (a multiple of 2048, at most kSymBits), so a matrix narrower
+    // than 2^20 columns takes a smaller bitmap and several blocks per CU
+    const uint32_t SB = f.sym_bits, kWords = SB / 32;
     // dynamic LDS only (16-byte aligned carve): bitmap | block-scan words | chunk-mask words
     extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
     uint32_t *sh = bits + kWords;
@@ -309,8 +311,8 @@ __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
         const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
         uint64_t count = 0;
         unsigned long long cm = 0;
-        for (uint64_t lo = 0; lo < p.ncols; lo += kSymBits) {
-            const uint32_t hi = (uint32_t)min<uint64_t>(p.ncols, lo + kSymBits);
+        for (uint64_t lo = 0; lo < p.ncols; lo += SB) {
+            const uint32_t hi = (uint32_t)min<uint64_t>(p.ncols, lo + SB);
             const bool all = lo == 0 && hi == p.ncols;
             fr_walk<uint32_t, false, I>(p, a0, a1, (uint32_t)lo, hi, all, [&](uint32_t c, uint32_t, uint32_t) {
                 const uint32_t o = c - (uint32_t)lo;
@@ -656,12 +658,18 @@ slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
 
 slat_status slat_fat_symbolic(slat_ctx *ctx, FatArgs &f, const Args &a, bool idx32) {
     f.a = a;
-    const dim3 g((unsigned)ctx->cu_count);
-    const size_t lds = kSymBits / 8 + kFW * 4 + kFW * 8;
+    // the bitmap covers min(2^20, columns rounded up to 2048) per pass; narrower matrices fit more
+    // blocks per CU (SLAT_FAT_SYM_FULL=1: always 2^20, one block per CU)
+    static const bool kFull = std::getenv("SLAT_FAT_SYM_FULL") != nullptr;
+    const uint64_t sb = kFull ? kSymBits : std::min<uint64_t>(kSymBits, (a.ncols + 2047) / 2048 * 2048);
+    f.sym_bits = (uint32_t)sb;
+    const size_t lds = sb / 8 + kFW * 4 + kFW * 8, lds_max = kSymBits / 8 + kFW * 4 + kFW * 8;
+    const unsigned per_cu = (unsigned)std::max<size_t>(1, std::min<size_t>(4, (160u * 1024u) / lds));
+    const dim3 g((unsigned)ctx->cu_count * per_cu);
     static std::atomic<uint64_t> attr{0};  // devices whose attribute is set (idempotent, so a race is harmless)
     if (!(attr.load(std::memory_order_relaxed) >> (ctx->device & 63) & 1)) {  // > 64 KB of dynamic LDS per block
-        (void)hipFuncSetAttribute((const void *)k_fr_symbolic<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute((const void *)k_fr_symbolic<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void *)k_fr_symbolic<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max);
+        (void)hipFuncSetAttribute((const void *)k_fr_symbolic<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max);
         attr.fetch_or(1ull << (ctx->device & 63), std::memory_order_relaxed);
     }
     if (idx32)

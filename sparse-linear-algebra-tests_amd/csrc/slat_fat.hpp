@@ -29,6 +29,7 @@ struct FatArgs {
     // counter instead of a fixed stride over the blocks
     unsigned long long *tq;
     uint64_t fat_min;  // products per row from which a row is fat (slat_fat_min())
+    uint32_t sym_bits;  // k_fr_symbolic's bitmap columns per pass (slat_fat_symbolic)
 };
 }  // namespace slat
 
