@@ -77,6 +77,10 @@ typedef enum { SLAT_DEVICE = 0, SLAT_HOST = 1 } slat_residency;
 /* the regular multi-kernel pipeline even for a small product (which otherwise runs as one kernel,
  * slat_tiny.hip); results are identical either way (tests run both) */
 #define SLAT_FLAG_NO_TINY 0x20u
+/* fat rows (MAGNUS's coarse category, >= 8192 products) accumulate from their products bucketed by
+ * accumulator chunk in HBM (MAGNUS's fine-level reordering) instead of per-chunk walks over B split by
+ * chunk, the default, which measured faster; results are identical */
+#define SLAT_FLAG_FAT_BUCKETS 0x40u
 
 typedef struct slat_ctx slat_ctx;
 

@@ -29,7 +29,7 @@
 using namespace slat;
 
 // max(B) for the CSR walk too (SLAT_NO_NARROW_CSR=1: the u64 slots of before, for A/B runs)
-static const bool kNarrowCsr = std::getenv("SLAT_NO_NARROW_CSR") == nullptr;
+static const bool kNarrowCsr = slat_ab_knob("SLAT_NO_NARROW_CSR") == nullptr;
 static void dev_release_all(slat_ctx *ctx);
 
 extern "C" {
@@ -57,7 +57,7 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SLAT_ENODEV;
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SLAT_ENODEV;
-    if (const char *e_ = std::getenv("SLAT_SPIN"))  // experiment: spin-wait stream syncs
+    if (const char *e_ = slat_ab_knob("SLAT_SPIN"))  // experiment: spin-wait stream syncs
         if (std::atoi(e_)) {
             (void)hipSetDevice(device);
             (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
@@ -488,7 +488,7 @@ static void pick_window(uint64_t ncols, uint32_t threads, uint32_t max_ww, uint3
 struct HostClock {
     static constexpr int kN = 9;
     static bool on() {
-        static const bool e = std::getenv("SLAT_HOST_CLOCK") != nullptr;
+        static const bool e = slat_ab_knob("SLAT_HOST_CLOCK") != nullptr;
         return e;
     }
     std::chrono::steady_clock::time_point t;
@@ -530,8 +530,8 @@ __global__ void k_signal(unsigned long long *word, unsigned long long v) {
 // hipStreamWriteValue64 instead of k_signal (A/B only).
 static int wait_mode() {
     static const int mode = [] {
-        const char *e = std::getenv("SLAT_WAIT");
-        if (std::getenv("SLAT_BLOCKING_SYNC") || (e && !std::strcmp(e, "sync"))) return 1;
+        const char *e = slat_ab_knob("SLAT_WAIT");
+        if (slat_ab_knob("SLAT_BLOCKING_SYNC") || (e && !std::strcmp(e, "sync"))) return 1;
         if (e && !std::strcmp(e, "write")) return 3;  // the sequence word stored by a stream write op
         return e && !std::strcmp(e, "query") ? 2 : 0;
     }();
@@ -660,7 +660,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // environment knobs (A/B experiments only) are read once: a getenv per call is host time on
     // every call
     static const uint32_t ablate = [] {  // experiments only: never reaches the real pipeline's kernels
-        const char *e = std::getenv("SLAT_ABLATE");
+        const char *e = slat_ab_knob("SLAT_ABLATE");
         return e ? (uint32_t)std::atoi(e) : 0u;
     }();
     Args asym = a;
@@ -673,7 +673,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // Wide launches (columns beyond one window) split the rows by MAGNUS-style category into two
     // launches per pass: short rows in a per-wave LDS hash table (mode 1), the rest by row-span
     // windows (mode 2; numeric windows of 1024 words keep two blocks per CU).
-    static const bool kNoHash = std::getenv("SLAT_NO_HASH") != nullptr;
+    static const bool kNoHash = slat_ab_knob("SLAT_NO_HASH") != nullptr;
     const bool hash = asym.wide && !kNoHash;
     if (hash) {
         a.ww = std::min<uint32_t>(a.ww, 1024);
@@ -687,13 +687,13 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // pipeline: profiles/r03_small_cells_tiny_abi.csv), 32-bit offsets, a wave per row with every row in flight, a product bound a wave
     // finishes in microseconds, no fat rows, and no per-pass timing or stats (those report the
     // regular pipeline's passes)
-    static const bool kNoTiny = std::getenv("SLAT_NO_TINY") != nullptr;
+    static const bool kNoTiny = slat_ab_knob("SLAT_NO_TINY") != nullptr;
     const bool tiny = !kNoTiny && !asym.wide && ncols <= 8192 && n <= 2048 && idx32 && wait_mode() == 0 && !ablate &&
                       !(flags & (SLAT_FLAG_TIMING | SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) &&
                       g_progress.load(std::memory_order_relaxed) == 0 &&
                       (unsigned __int128)a_nnz_block * maxrow_b <= (1u << 18) &&
                       (A->max_row_nnz ? (unsigned __int128)A->max_row_nnz * maxrow_b < slat_fat_min() : maxrow_b <= 32);
-    static const bool kNoEll = std::getenv("SLAT_NO_ELL") != nullptr;
+    static const bool kNoEll = slat_ab_knob("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
                      !kNoEll && !tiny;  // 24-bit row index, 31-bit byte offsets in the kernels
@@ -702,7 +702,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // rows; measured faster than oversubscribing); symbolic takes up to 16 blocks per CU.
     const int wpb = kBlock / kWave;
     static const int kCap = [] {  // tuning knob: rank slots per wave
-        const char *e = std::getenv("SLAT_CAP");
+        const char *e = slat_ab_knob("SLAT_CAP");
         return e ? std::max(64, std::atoi(e)) : 0;
     }();
     if (kCap) a.area = 6 * kCap;
@@ -711,7 +711,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // short rows batched several per hash table (integer semirings with the ELL copy of B), else
     // one row per table; composite (row, column) keys need the column bits + 6 <= 31
     // symbolic batches for every value type (it never reads values); numeric for the integer ones
-    static const bool kNoBatch = std::getenv("SLAT_NO_BATCH") != nullptr;
+    static const bool kNoBatch = slat_ab_knob("SLAT_NO_BATCH") != nullptr;
     const bool sym_batched = hash && ell && !kNoBatch;
     const bool batched = sym_batched && (dt != SLAT_F64 || f64any);
     if (sym_batched) {
@@ -729,13 +729,13 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const uint64_t row_blocks = (n + wpb - 1) / wpb;
     // grid geometry knobs (A/B only): symbolic blocks per CU, numeric oversubscription factor
     static const uint64_t kSymBpc = [] {
-        const char *e = std::getenv("SLAT_SYM_BPC");
+        const char *e = slat_ab_knob("SLAT_SYM_BPC");
         return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 16ull;
     }();
     // (the batched short-row tiles: twice the resident blocks, so blocks that drew cheap tiles
     // make room for more: C4 numeric 1.00 -> 0.91 ms, profiles/r03_ab_dyn_xlane.txt)
     static const uint64_t kNumOver = [] {
-        const char *e = std::getenv("SLAT_NUM_OVER");
+        const char *e = slat_ab_knob("SLAT_NUM_OVER");
         return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 2ull;
     }();
     const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * kSymBpc)));
@@ -768,7 +768,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         ctx->mem_changed = false;
     }
     const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
-    static const bool kNoSbm = std::getenv("SLAT_NO_SBM") != nullptr;
+    static const bool kNoSbm = slat_ab_knob("SLAT_NO_SBM") != nullptr;
     const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny;
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
@@ -778,7 +778,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const size_t o_l1 = o_smask + smask_b, o_l2 = o_l1 + list_b, o_lc = o_l2 + list_b, lc_b = sym_batched ? 256 : 0;
     // fat rows (MAGNUS's dense-accumulation category) once a row can reach slat_fat_min() products:
     // max row of A x max row of B (A's max row unknown: when B has long rows)
-    static const bool kNoFat = std::getenv("SLAT_NO_FAT") != nullptr;
+    static const bool kNoFat = slat_ab_knob("SLAT_NO_FAT") != nullptr;
     const uint64_t maxrow_a = A->max_row_nnz;
     const bool fat = !kNoFat && !tiny && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= slat_fat_min() : maxrow_b > 32);
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
@@ -839,7 +839,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // wide launches with B in CSR form: B bucketed by the window passes' column chunk (32 chunks over
     // the columns, 2^chunk_shift each), so a window walks only its chunks' part of each B row
     uint32_t *wsplit = nullptr;
-    static const bool kNoWinSplit = std::getenv("SLAT_NO_WIN_SPLIT") != nullptr;  // A/B knob
+    static const bool kNoWinSplit = slat_ab_knob("SLAT_NO_WIN_SPLIT") != nullptr;  // A/B knob
     if (hash && !ell && !kNoWinSplit && B->nnz) {
         uint32_t csh = 0;
         while (csh < 58 && ((ncols - 1) >> (csh + 5))) ++csh;
@@ -847,7 +847,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         const uint64_t nch1 = ((ncols + (1ull << csh) - 1) >> csh) + 1;
         if (B->n_rows * nch1 * 4 <= (256ull << 20) &&
             slat_dev_alloc(ctx, (void **)&wsplit, B->n_rows * nch1 * 4, s) == hipSuccess) {
-            SLAT_HIP(ctx, slat_launch_splits(ctx, B->row_ptr, B->col_idx, B->n_rows, (uint32_t)nch1, csh, wsplit, s));
+            if (slat_launch_splits(ctx, B->row_ptr, B->col_idx, B->n_rows, (uint32_t)nch1, csh, wsplit, s) != hipSuccess) {
+                ctx->err = "slat_launch_splits failed";
+                slat_dev_free(ctx, wsplit, s);
+                return SLAT_EHIP;
+            }
             a.wsplit = wsplit;
             a.wnch1 = (uint32_t)nch1;
         } else {
@@ -864,7 +868,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // and at most kBoundBytes: a loose bound (power-law B: nnz(A) x a hub row) would make every call
     // allocate and release tens of GB, which costs far more than the exact path's one sync
     static const uint64_t kBoundBytes = [] {
-        const char *e = std::getenv("SLAT_BOUND_MAX_BYTES");
+        const char *e = slat_ab_knob("SLAT_BOUND_MAX_BYTES");
         return e ? std::strtoull(e, nullptr, 10) : (4ull << 30);
     }();
     const unsigned __int128 budget = std::min<unsigned __int128>(ctx->free_b / 4, kBoundBytes);
@@ -937,6 +941,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     slat::FatArgs *fa = &fat_args;
     if (fat) {
         if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return failc(st);
+        fa->buckets = (flags & SLAT_FLAG_FAT_BUCKETS) ? 1u : 0u;
         asym.fr_mark = a.fr_mark;
     }
     if (ablate & 7u) {
@@ -954,7 +959,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // short-row tiles keep a fixed stride (tickets measured slower there).
     // SLAT_DYN=0: no tickets (A/B knob)
     static const uint32_t kDyn = [] {
-        const char *e = std::getenv("SLAT_DYN");
+        const char *e = slat_ab_knob("SLAT_DYN");
         return e ? (uint32_t)std::atoi(e) : 2u;
     }();
     unsigned long long *tq = ctx->d_words + 5;
@@ -1002,8 +1007,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         C->capacity = std::max<uint64_t>(total, 1);
         if (slat_dev_alloc(ctx, (void **)&C->col_idx, C->capacity * 4, s) != hipSuccess ||
             slat_dev_alloc(ctx, &C->values, C->capacity * vs, s) != hipSuccess) {
-            slat_csr_free(ctx, C);
-            return fail(ctx, SLAT_EOOM, "C allocation failed");
+            (void)hipGetLastError();
+            return failc(fail(ctx, SLAT_EOOM, "C allocation failed"));
         }
         if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
     }
@@ -1030,7 +1035,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.tq = (kDyn & 2u) && hash ? tq : nullptr;
     // the window pass is the call's last kernel unless fat rows or the stats copy follow: it stores
     // the completion word itself (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
-    static const bool kFusedSignal = std::getenv("SLAT_NO_FUSED_SIGNAL") == nullptr;
+    static const bool kFusedSignal = slat_ab_knob("SLAT_NO_FUSED_SIGNAL") == nullptr;
     if (kFusedSignal && !fat && !a.stats && wait_mode() == 0) {
         a.seq = ++ctx->done_seq;
         a.done = ctx->d_words + 6;

@@ -25,6 +25,10 @@
 struct slat_comm {
     ncclComm_t nc = nullptr;
     int nranks = 1, rank = 0, device = 0;
+    // device words of the collectives' own metadata, allocated with the communicator so no rank can
+    // fail an allocation between entering a call and reaching its first collective:
+    // [0, 8) status agreement and broadcast shape, [8, 8 + 5 (P + 1)) the allgather's block metadata
+    uint64_t *scratch = nullptr;
 };
 
 namespace {
@@ -125,9 +129,14 @@ extern "C" slat_status slat_comm_create(slat_ctx *ctx, int nranks, int rank, con
     c->nranks = nranks;
     c->rank = rank;
     c->device = ctx->device;
+    if (hipMalloc((void **)&c->scratch, (size_t)(8 + 5 * (nranks + 1)) * 8) != hipSuccess) {
+        delete c;
+        return fail(ctx, SLAT_EOOM, "communicator scratch allocation failed");
+    }
     const ncclResult_t r = ncclCommInitRank(&c->nc, nranks, u, rank);
     if (r != ncclSuccess) {
         ctx->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+        (void)hipFree(c->scratch);
         delete c;
         return SLAT_EHIP;
     }
@@ -138,6 +147,7 @@ extern "C" slat_status slat_comm_create(slat_ctx *ctx, int nranks, int rank, con
 extern "C" slat_status slat_comm_destroy(slat_comm *comm) {
     if (!comm) return SLAT_EINVAL;
     if (comm->nc) (void)ncclCommDestroy(comm->nc);
+    if (comm->scratch) (void)hipFree(comm->scratch);
     delete comm;
     return SLAT_OK;
 }
@@ -194,18 +204,13 @@ namespace {
 // allocate must not leave the others blocked inside broadcasts it never joins
 slat_status agree(slat_ctx *ctx, slat_comm *comm, slat_status mine) {
     const hipStream_t s = ctx->stream;
-    uint32_t *w = nullptr;
-    if (slat_dev_alloc(ctx, (void **)&w, 8, s) != hipSuccess) {
-        // cannot even agree: report this rank's failure (the others see RCCL's own timeout)
-        return mine != SLAT_OK ? mine : fail(ctx, SLAT_EOOM, "status word allocation failed");
-    }
+    uint32_t *w = (uint32_t *)comm->scratch;  // allocated with the communicator: no failure here
     uint32_t v = (uint32_t)mine, got = 0;
     slat_status st = SLAT_OK;
     if (hipMemcpyAsync(w, &v, 4, hipMemcpyHostToDevice, s) != hipSuccess) st = SLAT_EHIP;
     SLAT_NCCL_KEEP(ctx, st, ncclAllReduce(w, w + 1, 1, ncclUint32, ncclMax, comm->nc, s));
     if (hipMemcpyAsync(&got, w + 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
         st = SLAT_EHIP;
-    slat_dev_free(ctx, w, s);
     if (st != SLAT_OK) return st;
     if (got != SLAT_OK && mine == SLAT_OK) return fail(ctx, (slat_status)got, "another rank failed");
     return (slat_status)got;
@@ -291,15 +296,13 @@ extern "C" slat_status slat_bcast_csr(slat_ctx *ctx, slat_comm *comm, slat_csr *
     const hipStream_t s = ctx->stream;
     // shape first: (rows, cols, nnz, dtype, max row) from the root
     uint64_t meta[5] = {m->n_rows, m->n_cols, m->nnz, (uint64_t)m->dtype, m->max_row_nnz};
-    uint64_t *dmeta = nullptr;
-    SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&dmeta, sizeof meta, s));
+    uint64_t *dmeta = comm->scratch + 2;  // words 2..6 (0..1: the status agreement)
     slat_status st = SLAT_OK;
     if (hipMemcpyAsync(dmeta, meta, sizeof meta, hipMemcpyHostToDevice, s) != hipSuccess) st = fail(ctx, SLAT_EHIP, "meta upload");
     SLAT_NCCL_KEEP(ctx, st, ncclBroadcast(dmeta, dmeta, 5, ncclUint64, root, comm->nc, s));
     if (hipMemcpyAsync(meta, dmeta, sizeof meta, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         if (st == SLAT_OK) st = fail(ctx, SLAT_EHIP, "meta read-back");
-    slat_dev_free(ctx, dmeta, s);
     if (st != SLAT_OK) return st;
     const int32_t dt = (int32_t)meta[3];
     if (dt < SLAT_U32 || dt > SLAT_F64) return fail(ctx, SLAT_EINVAL, "broadcast matrix: bad dtype");  // on every rank
@@ -348,25 +351,34 @@ extern "C" slat_status slat_allgather_rows(slat_ctx *ctx, slat_comm *comm, const
     const int32_t dt = vst == SLAT_OK ? block->dtype : -1;
     // every block's (rows, nnz, max row, dtype); a block's row_ptr may be a view into a larger matrix
     // (absolute offsets), so its entries are taken relative to row_ptr[0]
+    // (a failed read of it also travels as an invalid dtype: no rank returns before the gather)
     uint64_t first = 0;
-    if (vst == SLAT_OK && block->n_rows) SLAT_HIP(ctx, hipMemcpyAsync(&first, block->row_ptr, 8, hipMemcpyDeviceToHost, s));
-    SLAT_HIP(ctx, hipStreamSynchronize(s));
-    const uint64_t mine[4] = {vst == SLAT_OK ? block->n_rows : 0, vst == SLAT_OK ? block->nnz : 0,
-                              vst == SLAT_OK ? block->max_row_nnz : 0, (uint64_t)(int64_t)dt};
-    std::vector<uint64_t> all((size_t)4 * P);
-    uint64_t *dm = nullptr;
-    SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&dm, (size_t)(4 + 4 * P) * 8, s));
+    if (vst == SLAT_OK && block->n_rows &&
+        (hipMemcpyAsync(&first, block->row_ptr, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+         hipStreamSynchronize(s) != hipSuccess))
+        vst = fail(ctx, SLAT_EHIP, "block row_ptr read-back");
+    const int32_t dtm = vst == SLAT_OK ? dt : -1;
+    // (rows, nnz, max row, dtype, columns) of every block: the columns must agree on every rank
+    const uint64_t mine[5] = {vst == SLAT_OK ? block->n_rows : 0, vst == SLAT_OK ? block->nnz : 0,
+                              vst == SLAT_OK ? block->max_row_nnz : 0, (uint64_t)(int64_t)dtm,
+                              vst == SLAT_OK ? block->n_cols : 0};
+    std::vector<uint64_t> all5((size_t)5 * P), all((size_t)4 * P);
+    uint64_t *dm = comm->scratch + 8;  // allocated with the communicator
     slat_status st = SLAT_OK;
     if (hipMemcpyAsync(dm, mine, sizeof mine, hipMemcpyHostToDevice, s) != hipSuccess) st = fail(ctx, SLAT_EHIP, "meta upload");
-    SLAT_NCCL_KEEP(ctx, st, ncclAllGather(dm, dm + 4, 4, ncclUint64, comm->nc, s));
-    if ((hipMemcpyAsync(all.data(), dm + 4, all.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    SLAT_NCCL_KEEP(ctx, st, ncclAllGather(dm, dm + 5, 5, ncclUint64, comm->nc, s));
+    if ((hipMemcpyAsync(all5.data(), dm + 5, all5.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
          hipStreamSynchronize(s) != hipSuccess) && st == SLAT_OK)
         st = fail(ctx, SLAT_EHIP, "meta read-back");
-    slat_dev_free(ctx, dm, s);
     if (st != SLAT_OK) return st;
-    for (int r = 0; r < P; ++r)
-        if ((int32_t)all[4 * r + 3] < SLAT_U32 || (int32_t)all[4 * r + 3] > SLAT_F64)
+    for (int r = 0; r < P; ++r) {
+        for (int k = 0; k < 4; ++k) all[4 * r + k] = all5[5 * r + k];
+        if ((int32_t)all5[5 * r + 3] < SLAT_U32 || (int32_t)all5[5 * r + 3] > SLAT_F64)
             return vst != SLAT_OK ? vst : fail(ctx, SLAT_EINVAL, "another rank's block is malformed");
+    }
+    for (int r = 0; r < P; ++r)  // the same verdict on every rank: every rank saw the same words
+        if ((int32_t)all5[5 * r + 3] != (int32_t)all5[3] || all5[5 * r + 4] != all5[4])
+            return fail(ctx, SLAT_EDIM, "the row blocks differ in value type or columns");
     // every allocation before the data moves, then one agreed status
     Assembly a;
     uint64_t *my_ends_tmp = nullptr;
@@ -388,7 +400,10 @@ extern "C" slat_status slat_allgather_rows(slat_ctx *ctx, slat_comm *comm, const
     const uint8_t *my_col = (const uint8_t *)block->col_idx + first * 4;
     const uint8_t *my_val = (const uint8_t *)block->values + first * vsize(dt);
     SLAT_NCCL_KEEP(ctx, st, ncclGroupStart());
-    for (int r = 0; r < P && st == SLAT_OK; ++r) {
+    // every rank issues the same sequence of broadcasts whatever happened locally (an enqueue error
+    // is kept, the rest still issued, then the ranks agree): stopping early would leave the peers
+    // blocked inside broadcasts this rank never joined
+    for (int r = 0; r < P; ++r) {
         const uint64_t rows = all[4 * r], nz = all[4 * r + 1];
         const bool me = r == comm->rank;
         if (rows)
@@ -404,6 +419,7 @@ extern "C" slat_status slat_allgather_rows(slat_ctx *ctx, slat_comm *comm, const
     }
     SLAT_NCCL_KEEP(ctx, st, ncclGroupEnd());
     if (st == SLAT_OK) st = assembly_finish(ctx, a, full, P);
+    st = agree(ctx, comm, st);
     cleanup();
     if (st != SLAT_OK && full->row_ptr) {
         (void)hipStreamSynchronize(s);
@@ -443,8 +459,9 @@ extern "C" slat_status slat_concat_rows(slat_ctx *ctx, const slat_csr_view *bloc
         const slat_csr_view &b = blocks[r];
         const uint64_t *ends = nullptr;
         uint64_t *tmp = nullptr;
-        if ((st = rel_ends(ctx, &b, first[r], &ends, &tmp))) break;
-        if (tmp) tmps.push_back(tmp);
+        st = rel_ends(ctx, &b, first[r], &ends, &tmp);
+        if (tmp) tmps.push_back(tmp);  // freed below, also when rel_ends failed after allocating it
+        if (st) break;
         hipError_t e = hipSuccess;
         if (b.n_rows)
             e = hipMemcpyAsync(full->row_ptr + 1 + a.row_off[r], ends, b.n_rows * 8, hipMemcpyDeviceToDevice, s);

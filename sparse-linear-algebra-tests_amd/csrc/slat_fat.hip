@@ -604,7 +604,7 @@ using namespace slat;
 // 15.8 -> 13.7 ms, 2^18 fold 121 -> 114 ms, profiles/r03_ab_fat_min.txt; SLAT_FAT_MIN: A/B knob)
 uint64_t slat_fat_min() {
     static const uint64_t v = [] {
-        const char *e = std::getenv("SLAT_FAT_MIN");
+        const char *e = slat_ab_knob("SLAT_FAT_MIN");
         return e ? std::max<uint64_t>(256, std::strtoull(e, nullptr, 10)) : 8192ull;
     }();
     return v;
@@ -646,6 +646,7 @@ slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
     f.bcap = 0;
     f.tq = ctx->d_words + 5;
     f.fat_min = slat_fat_min();
+    f.buckets = 0;
     SLAT_HIP(ctx, hipMemsetAsync(f.cnt, 0, 4, s));
     a.fr_mark = f.mark;
     f.a = a;
@@ -660,7 +661,7 @@ slat_status slat_fat_symbolic(slat_ctx *ctx, FatArgs &f, const Args &a, bool idx
     f.a = a;
     // the bitmap covers min(2^20, columns rounded up to 2048) per pass; narrower matrices fit more
     // blocks per CU (SLAT_FAT_SYM_FULL=1: always 2^20, one block per CU)
-    static const bool kFull = std::getenv("SLAT_FAT_SYM_FULL") != nullptr;
+    static const bool kFull = slat_ab_knob("SLAT_FAT_SYM_FULL") != nullptr;
     const uint64_t sb = kFull ? kSymBits : std::min<uint64_t>(kSymBits, (a.ncols + 2047) / 2048 * 2048);
     f.sym_bits = (uint32_t)sb;
     const size_t lds = sb / 8 + kFW * 4 + kFW * 8, lds_max = kSymBits / 8 + kFW * 4 + kFW * 8;
@@ -682,7 +683,7 @@ slat_status slat_fat_symbolic(slat_ctx *ctx, FatArgs &f, const Args &a, bool idx
 
 // split tables above this size are not built (the walks then filter B rows by column range)
 static const uint64_t kSplitBytes = [] {
-    const char *e = std::getenv("SLAT_FAT_SPLIT_BYTES");
+    const char *e = slat_ab_knob("SLAT_FAT_SPLIT_BYTES");
     return e ? std::strtoull(e, nullptr, 10) : (256ull << 20);
 }();
 
@@ -699,7 +700,7 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
     // so no wave searches its slice in a B row)
     const uint64_t nb = h.a.b_nrows;
     uint32_t sh = (uint32_t)__builtin_ctz(fr_chunk<Sem>());
-    static const bool kNoSlices = std::getenv("SLAT_NO_FAT_SLICES") != nullptr;  // A/B knob
+    static const bool kNoSlices = slat_ab_knob("SLAT_NO_FAT_SLICES") != nullptr;  // A/B knob
     if (Sem::kOrdered && !kNoSlices) {
         const uint32_t fine = sh - (uint32_t)__builtin_ctz((uint32_t)kFW);
         const uint64_t ng = (h.a.ncols + (1ull << fine) - 1) >> fine;
@@ -710,7 +711,7 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
     h.split = nullptr;
     h.nch1 = 0;
     h.gsh = sh;
-    static const bool kNoSplit = std::getenv("SLAT_NO_FAT_SPLIT") != nullptr;  // A/B knob
+    static const bool kNoSplit = slat_ab_knob("SLAT_NO_FAT_SPLIT") != nullptr;  // A/B knob
     if (nch > 1 && nb * (nch + 1) * 4 <= kSplitBytes && !kNoSplit) {
         if (slat_dev_alloc(ctx, (void **)&split, nb * (nch + 1) * 4, ctx->stream) == hipSuccess) {
             const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb * (nch + 1) + kBlock - 1) / kBlock,
@@ -736,9 +737,8 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
     h.bcap = 0;
     // (off by default: with the long B rows' loads in flight together, the per-chunk walks over B split
     // by chunk beat the bucket scatter, which moves 4x the bytes: R-MAT 2^16 A^2 fat rows 7.4 GB /
-    // 6.9 ms against 1.8 GB / 3.6 ms, profiles/r03_fat_bucket_vs_rewalk.txt; SLAT_FAT_BUCKETS=1: on)
-    static const bool kBuckets = std::getenv("SLAT_FAT_BUCKETS") != nullptr;  // A/B knob
-    if (!Sem::kOrdered && kBuckets && (h.a.ncols + fr_chunk<Sem>() - 1) / fr_chunk<Sem>() <= kMaxBuckets) {
+    // 6.9 ms against 1.8 GB / 3.6 ms, profiles/r03_fat_bucket_vs_rewalk.txt; SLAT_FLAG_FAT_BUCKETS: on)
+    if (!Sem::kOrdered && f.buckets && (h.a.ncols + fr_chunk<Sem>() - 1) / fr_chunk<Sem>() <= kMaxBuckets) {
         const uint32_t cap = 1u << 19;
         const size_t nbk = (size_t)g.x * cap;
         if (slat_dev_alloc(ctx, (void **)&bcol, nbk * 4, ctx->stream) == hipSuccess &&

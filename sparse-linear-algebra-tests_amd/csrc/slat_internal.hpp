@@ -4,12 +4,26 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "slat.h"
+
+// A/B experiment knobs (environment variables) exist only in builds made with -DSLAT_AB_KNOBS
+// (tools/build_variant.sh adds it): the shipped libslat.so ignores the environment, so a stray
+// variable cannot change its kernel choices. (SLAT_MATMUL_PROGRESS, the reference's
+// MATMUL_PROGRESS switch, is a feature and is read by every build.)
+inline const char *slat_ab_knob(const char *name) {
+#ifdef SLAT_AB_KNOBS
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 
 struct slat_ctx {
     int device = 0;

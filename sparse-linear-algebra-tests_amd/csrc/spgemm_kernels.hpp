@@ -1798,8 +1798,11 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
                             const S *av = (const S *)p.a_val;
                             for (I j = j0 + (I)lane; j < a1; j += (I)kWave) am = max(am, sat32(av[j]));
                         }
-                        const uint64_t x = (uint64_t)wave_max_u32(am) * bvmax;
-                        narrow = x == 0 || len <= 0xFFFFFFFFull / x;
+                        const uint32_t wam = wave_max_u32(am);
+                        const uint64_t x = (uint64_t)wam * bvmax;
+                        // a 64-bit A value of 2^32 or more clamps to 0xFFFFFFFF in sat32: its true
+                        // size is unknown, so such a row never narrows (as for B's clamped max)
+                        narrow = (sizeof(S) == 4 || wam != 0xFFFFFFFFu) && (x == 0 || len <= 0xFFFFFFFFull / x);
                     }
                 }
                 // one rank chunk [r0, r0 + nch): zero its slots, accumulate, emit. R0: r0 == 0.

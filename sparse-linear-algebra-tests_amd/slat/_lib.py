@@ -14,6 +14,7 @@ SLAT_OK, SLAT_EINVAL, SLAT_EDIM, SLAT_EOOM, SLAT_EHIP, SLAT_ENOTSUP, SLAT_ENODEV
 U32, SAT64, F64 = 0, 1, 2
 DEVICE, HOST = 0, 1
 FLAG_TIMING, FLAG_EXACT_ALLOC, FLAG_STATS, FLAG_F64_ANY_ORDER, FLAG_IDX64, FLAG_NO_TINY = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+FLAG_FAT_BUCKETS = 0x40  # fat rows: products bucketed by accumulator chunk (MAGNUS fine-level reordering)
 
 # Every symbol include/slat.h declares (checked by tests/test_abi.py).
 EXPORTS = [

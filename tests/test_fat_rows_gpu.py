@@ -72,9 +72,11 @@ def test_f64_any_order_within_tolerance():
     np.testing.assert_allclose(got.values, wval, rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize("flags", [0, slat.FLAG_FAT_BUCKETS])
 @pytest.mark.parametrize("dtype", [O.U32, O.F64])
-def test_wide_fat_rows_past_2_20_columns(dtype):
-    """3M columns: symbolic passes of 2^20 columns, accumulator chunks skipped by the touched mask."""
+def test_wide_fat_rows_past_2_20_columns(dtype, flags):
+    """3M columns: symbolic passes of 2^20 columns, accumulator chunks skipped by the touched mask.
+    FLAG_FAT_BUCKETS: the same with MAGNUS's fine-level reordering (products bucketed by chunk)."""
     rng = np.random.default_rng(3)
     n, ncols = 64, 3_000_000
     # A: 64 x 64 dense-ish; B: 64 rows, each with 600 random columns spread over 3M
@@ -94,7 +96,7 @@ def test_wide_fat_rows_past_2_20_columns(dtype):
     out = slat._lib.CsrOwned()
     va = da.view()
     slat._lib.check(slat.lib().slat_spgemm(da._ctx.ptr, slat._lib.C.byref(va), slat._lib.C.byref(vb),
-                                           slat._lib.C.byref(out), 0), da._ctx.ptr)
+                                           slat._lib.C.byref(out), flags), da._ctx.ptr)
     got = cls(out, da._ctx).host()
     # exact restatement: dense rows of the product (small n)
     import scipy.sparse as sp
@@ -107,7 +109,8 @@ def test_wide_fat_rows_past_2_20_columns(dtype):
     np.testing.assert_array_equal(got.values.astype(np.float64), Cm.data)  # small integers: exact in f64
 
 
-def test_zeros_and_cancellation_in_fat_rows():
+@pytest.mark.parametrize("flags", [0, slat.FLAG_FAT_BUCKETS])
+def test_zeros_and_cancellation_in_fat_rows(flags):
     """Explicit zero inputs (u32) and exact f64 cancellation inside fat rows are dropped like
     CsrMatrix::matmul does (src/graph_csr.rs:334, linalg/src/csr.rs:344)."""
     a = rmat(11, 8, O.U32)
@@ -116,37 +119,11 @@ def test_zeros_and_cancellation_in_fat_rows():
     val[::7] = 0
     az = O.from_arrays(rp, col, val, O.U32)
     p2 = O.matmul_seq(a, a)
-    assert_same(to_dev(p2, slat.CsrMatrix)._spgemm(to_dev(az, slat.CsrMatrix)), O.matmul_seq(p2, az), "u32 zeros")
+    assert_same(to_dev(p2, slat.CsrMatrix)._spgemm(to_dev(az, slat.CsrMatrix), flags), O.matmul_seq(p2, az), "u32 zeros")
     f = rmat(11, 8, O.F64)
     frp, fcol, fval = f.arrays()
     fval = fval.copy()
     fval[1::2] *= -1.0  # signed values: sums can cancel exactly
     fs = O.from_arrays(frp, fcol, fval, O.F64)
     fp = O.matmul_seq(fs, fs)
-    assert_same(to_dev(fp, slat.CsrF64)._spgemm(to_dev(fs, slat.CsrF64)), O.matmul_seq(fp, fs), "f64 signs")
-
-
-def test_bucketed_products_knob():
-    """MAGNUS's fine-level reordering (the fat rows' products scattered by accumulator chunk into HBM,
-    then each chunk accumulated from its bucket) is off by default since round 3 (the per-chunk walks
-    over B split by chunk measured faster); SLAT_FAT_BUCKETS=1 turns it on. The
-    knob is read once per process, so the bucketed path runs in a child process here, against the
-    oracle, on the wide fat rows (3M columns, many chunks per row) and the zeros / cancellation case."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = """
-import sys
-sys.path[:0] = [{pkg!r}, {orc!r}, {tests!r}]
-import oracle_py as O
-import test_fat_rows_gpu as T
-for dt in (O.U32, O.F64):  # 3M columns: fat rows spanning many accumulator chunks take the buckets
-    T.test_wide_fat_rows_past_2_20_columns(dt)
-T.test_zeros_and_cancellation_in_fat_rows()
-print("ok")
-""".format(pkg=os.path.join(root, "sparse-linear-algebra-tests_amd"), orc=os.path.join(root, "oracle"),
-           tests=os.path.join(root, "tests"))
-    env = dict(os.environ, SLAT_FAT_BUCKETS="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
+    assert_same(to_dev(fp, slat.CsrF64)._spgemm(to_dev(fs, slat.CsrF64), flags), O.matmul_seq(fp, fs), "f64 signs")

@@ -386,3 +386,28 @@ def test_long_rows_narrow_bound_stored_bitmap(ctx, dtype, vbig):
     R, Cc, Vv = R[first], Cc[first], Vv[first]
     a = O.from_coo(n, R, Cc, Vv.astype(np.uint32) if dtype == slat.U32 else Vv, DT[dtype])
     assert_same(to_dev(a, dtype)._spgemm(to_dev(a, dtype)), O.matmul_seq(a, a), f"long rows vbig={vbig}")
+
+
+@pytest.mark.parametrize("b_form", ["ell", "csr"])
+@pytest.mark.parametrize("n", [3000, 70000])
+def test_sat64_narrow_bound_clamped_a_values(ctx, b_form, n):
+    """Sat64 A values of 2^32 and more against a 0/1 pattern B. The narrow-slot bound sees A values
+    clamped to u32 (0xFFFFFFFF), so a one-entry row with bound 0xFFFFFFFF * 1 * 1 < 2^32 must still
+    take wide slots: in u32 slots 2^32 + 5 became 5 and 2^32 became 0 (dropped as a zero).
+    b_form: B rows of <= 32 entries (the ELL image) or a 40-entry row (B walked in CSR form);
+    n = 70000 is a wide launch (columns past one LDS window)."""
+    rng = np.random.default_rng(7)
+    big = np.array([1 << 32, (1 << 32) + 5, (1 << 33) + 1, 0xFFFFFFFF, 1, (1 << 63) + 3], np.uint64)
+    ar = np.arange(0, n, 3, dtype=np.int64)  # one entry per listed A row
+    ac = rng.integers(0, n, len(ar))
+    av = big[np.arange(len(ar)) % len(big)]
+    a = O.from_coo(n, ar, ac, av, O.SAT64)
+    br, bc = [], []
+    for r in range(n):
+        k = 40 if (b_form == "csr" and r % 500 == 0) else int(rng.integers(1, 6))
+        br.append(np.full(k, r)), bc.append(rng.choice(n, k, replace=False))
+    R, Cc = np.concatenate(br), np.concatenate(bc)
+    b = O.from_coo(n, R, Cc, np.ones(len(R), np.uint64), O.SAT64)
+    for flags in (0, slat.FLAG_NO_TINY):
+        got = to_dev(a, slat.SAT64)._spgemm(to_dev(b, slat.SAT64), flags)
+        assert_same(got, O.matmul_seq(a, b), f"Sat64 clamped A max, B {b_form}, n={n}, flags={flags}")

@@ -5,4 +5,4 @@
 set -e
 root="$(cd "$(dirname "$0")/.." && pwd)"
 mkdir -p "$root/tools/var"
-make -s -j8 -C "$root/sparse-linear-algebra-tests_amd" BUILD=/tmp/slat_var_$1 "EXTRA=$2" OUT="$root/tools/var/libslat_$1.so"
+make -s -j8 -C "$root/sparse-linear-algebra-tests_amd" BUILD=/tmp/slat_var_$1 "EXTRA=-DSLAT_AB_KNOBS $2" OUT="$root/tools/var/libslat_$1.so"
