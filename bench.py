@@ -58,7 +58,7 @@ def build_inputs(side: int, power: int, ctx):
     return A, P
 
 
-def cpu_baseline(side: int, power: int, seconds: float = 12.0):
+def cpu_baseline(side: int, power: int, seconds: float = 12.0):  # noqa: C901
     """Oracle restatement of CsrMatrix::matmul_par (oracle/, kind 'port') on this host's cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as O
@@ -78,17 +78,70 @@ def cpu_baseline(side: int, power: int, seconds: float = 12.0):
         if (el >= seconds and iters >= 3) or iters >= 200:
             break
     per = el / iters
-    return {"value": nnz / per / 1e9, "unit": "GNNZ/s", "cores": threads, "kind": "port",
+    return {"value": nnz / per / 1e9, "unit": "GNNZ/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"A^{power - 1}*A on {side}^3 torus (nnz(C)={nnz}), {iters} timed calls after 1 warm-up, "
                       f"{per * 1e3:.2f} ms/call, oracle/oracle.c orc_matmul_par with {threads} threads"}
 
 
 def load_pmc(workload: str):
-    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if os.path.exists(p):
-        with open(p) as f:
-            return json.load(f)
-    return None
+    """The newest round's counter summary of the headline kernel, profiles/rNN_pmc_<workload>.json
+    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, tools/pmc_headline.py), and its
+    file name; the bench itself cannot run under --pmc and time at once."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]*_pmc_{workload}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], ROOT)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def e2e_leg(ctx, P, A, steps: int):
+    """The host-resident call the drop-in makes (CsrMatrix::matmul over Vecs, graph_magnus.rs:758-772
+    times it that way): H2D of both operands, the product, D2H of C into fresh host arrays, the device
+    result freed. Pageable numpy arrays, then page-locked ones (inputs and an output pool allocated
+    once, outside the timed calls, as a binding would keep them)."""
+    hP, hA = P.host(), A.host()
+    hP = slat.HostCsr(hP.n, hP.row_ptr, hP.col_idx, hP.values, hP.dtype)  # plain copies, no device link
+    out = {}
+    nnz = [0]
+
+    def run_pageable():
+        nnz[0] = slat.spgemm_host(hP, hA, ctx).nnz
+
+    def pin(x):
+        y = slat.pinned_empty(len(x), x.dtype)
+        y[:] = x
+        return y
+    pP = slat.HostCsr(hP.n, pin(hP.row_ptr), pin(hP.col_idx), pin(hP.values), hP.dtype)
+    pA = slat.HostCsr(hA.n, pin(hA.row_ptr), pin(hA.col_idx), pin(hA.values), hA.dtype)
+    pool = {}
+
+    def pooled(n, dt):  # a pinned output pool, one buffer per (array, size), reused across calls
+        key = (n, np.dtype(dt).str)
+        if key not in pool:
+            pool[key] = slat.pinned_empty(n, dt)
+        return pool[key]
+
+    def run_pinned():
+        nnz[0] = slat.spgemm_host(pP, pA, ctx, alloc=pooled).nnz
+
+    for name, fn in (("pageable", run_pageable), ("pinned", run_pinned)):
+        fn()  # warm-up (and the pinned pool)
+        el = timed_steps(fn, steps, 1, ctx.sync)
+        out[name] = (el / steps * 1e3, nnz[0] * steps / el / 1e9)
+    return out
 
 
 def golden(side: int, power: int):
@@ -218,6 +271,7 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 strong-scaling leg")
     ap.add_argument("--c4-steps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--e2e-steps", type=int, default=10, help="host-resident calls timed per mode (0: skip)")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="record the per-kernel HIP events (roofline) on every k-th timed step; the event "
                          "records cost host time, so the other steps run without them")
@@ -304,6 +358,7 @@ def main():
         ok = torch.tensor([0 if par is False else 1], dtype=torch.int32, device=coll_dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     nnz_a = P.nnz()
+    e2e = e2e_leg(ctx, P, A, args.e2e_steps) if (rank == 0 and args.e2e_steps > 0) else None
     del P
 
     if c4 is None and not args.no_c4:
@@ -312,20 +367,22 @@ def main():
     if comm is not None:
         comm.close()
     if rank == 0:
-        emit(args, world, side, power, n, nnz_a, A.nnz(), nnz_c, value, ms_per_step, stats, sym, scan, num, tot, abl, par, c4)
+        emit(args, world, side, power, n, nnz_a, A.nnz(), nnz_c, value, ms_per_step, stats, sym, scan, num, tot, abl, par, c4,
+             e2e)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def emit(args, world, side, power, n, nnz_a, nnz_b, nnz_c, value, ms_per_step, stats, sym, scan, num, tot, abl, par, c4):
+def emit(args, world, side, power, n, nnz_a, nnz_b, nnz_c, value, ms_per_step, stats, sym, scan, num, tot, abl, par, c4,
+         e2e=None):
     alg = algorithmic_bytes(nnz_a, nnz_b, nnz_c, n, 4)
     num_ms = float(np.mean(num))
     achieved = alg / (max(num_ms, 1e-6) * 1e-3) / 1e9
-    pmc = load_pmc(f"torus{side}_a{power}")
+    pmc, pmc_file = load_pmc(f"torus{side}_a{power}")
     traffic = pmc.get("numeric_bytes_per_launch") if pmc else None
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_file": pmc_file,
                 "kernel": "k_numeric", "algorithmic_bytes": alg, "timed_steps": len(num),
                 "kernel_ms": {"symbolic": round(float(np.mean(sym)), 4), "scan": round(float(np.mean(scan)), 4),
                               "numeric": round(num_ms, 4), "device_total": round(float(np.mean(tot)), 4)},
@@ -351,7 +408,15 @@ def emit(args, world, side, power, n, nnz_a, nnz_b, nnz_c, value, ms_per_step, s
                    "capacity": stats["capacity"], "mode": stats["mode"], "window_words": stats["window_words"],
                    **({"ablated_ms": round(float(np.mean(abl)), 4)} if os.environ.get("SLAT_ABLATE") else {}),
                    **({"c4": c4} if c4 is not None else {}),
-                   **({"c4_single_gpu_ms": c4.get("single_gpu_ms")} if c4 is not None else {})},
+                   # the C4 strong-scaling figures again as top-level scalars (a nested dict may not
+                   # survive a flat parse of the line)
+                   **({"c4_ms_per_step": c4.get("ms_per_step"), "c4_gnnz_per_s": c4.get("gnnz_per_s"),
+                       "c4_single_gpu_ms": c4.get("single_gpu_ms"), "c4_speedup": c4.get("speedup"),
+                       "c4_gather_ms": c4.get("gather_ms"), "c4_parity": c4.get("parity")} if c4 is not None else {}),
+                   # host-resident calls (PCIe both ways: the drop-in's cost for Vec in / Vec out)
+                   **({"e2e_ms": round(e2e["pageable"][0], 4), "e2e_gnnz_per_s": round(e2e["pageable"][1], 4),
+                       "e2e_pinned_ms": round(e2e["pinned"][0], 4),
+                       "e2e_pinned_gnnz_per_s": round(e2e["pinned"][1], 4)} if e2e else {})},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

@@ -368,6 +368,10 @@ slat_status slat_spgemm_dense(slat_ctx *ctx, const slat_csr_view *A, const slat_
 slat_status slat_device_alloc(slat_ctx *ctx, uint64_t bytes, void **p);
 slat_status slat_device_free(slat_ctx *ctx, void *p);
 slat_status slat_device_copy(slat_ctx *ctx, void *dst, const void *src, uint64_t bytes, int32_t to_host);
+/* Page-locked host memory (hipHostMalloc): host views and slat_csr_to_host destinations in such
+ * buffers move over PCIe by DMA at full rate; pageable buffers are staged by the runtime. */
+slat_status slat_host_alloc(uint64_t bytes, void **p);
+slat_status slat_host_free(void *p);
 
 
 #ifdef __cplusplus

@@ -146,6 +146,17 @@ slat_csr_view slat_csr_view_of(const slat_csr *m) {
     return v;
 }
 
+slat_status slat_host_alloc(uint64_t bytes, void **p) {
+    if (!p) return SLAT_EINVAL;
+    *p = nullptr;
+    return hipHostMalloc(p, std::max<uint64_t>(bytes, 1), hipHostMallocDefault) == hipSuccess ? SLAT_OK : SLAT_EOOM;
+}
+
+slat_status slat_host_free(void *p) {
+    if (!p) return SLAT_OK;
+    return hipHostFree(p) == hipSuccess ? SLAT_OK : SLAT_EINVAL;
+}
+
 slat_status slat_csr_free(slat_ctx *ctx, slat_csr *m) {
     if (!ctx || !m) return SLAT_EINVAL;
     (void)hipSetDevice(ctx->device);

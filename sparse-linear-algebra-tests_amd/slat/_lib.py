@@ -32,7 +32,8 @@ EXPORTS = [
     "slat_magnus_add", "slat_magnus_reachability_sum", "slat_magnus_power_until_stable",
     "slat_magnus_connected_components",
     "slat_comm_id", "slat_comm_create", "slat_comm_destroy", "slat_rowblock_cuts", "slat_bcast_csr",
-    "slat_allgather_rows", "slat_concat_rows", "slat_diameter", "slat_spgemm_btree",
+    "slat_allgather_rows", "slat_concat_rows", "slat_diameter", "slat_spgemm_btree", "slat_host_alloc",
+    "slat_host_free",
 ]
 
 
@@ -177,6 +178,8 @@ def lib():
         "slat_concat_rows": ([vp, P(CsrView), C.c_uint32, P(CsrOwned)], C.c_int),
         "slat_diameter": ([vp, P(CsrView), P(u64), P(u64), P(u64)], C.c_int),
         "slat_spgemm_btree": ([vp, P(BTreeView), P(BTreeView), P(CsrOwned), u32], C.c_int),
+        "slat_host_alloc": ([u64, P(vp)], C.c_int),
+        "slat_host_free": ([vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

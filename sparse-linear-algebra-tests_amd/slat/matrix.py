@@ -210,6 +210,54 @@ def torus_thinned_device(side: int, epn: float, rng: StdRng, ctx: Context | None
 
 
 # ------------------------------------------------------------------------------------------------
+# host-resident products (the reference's Vec in / Vec out calls, PCIe included)
+# ------------------------------------------------------------------------------------------------
+class _PinnedBuf:
+    """Page-locked host bytes (slat_host_alloc), freed with the last array that views them."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = C.c_void_p()
+        L.check(L.lib().slat_host_alloc(max(int(nbytes), 1), C.byref(self.ptr)))
+        self.__array_interface__ = {"shape": (max(int(nbytes), 1),), "typestr": "|u1",
+                                    "data": (self.ptr.value, False), "version": 3}
+
+    def __del__(self):
+        try:
+            L.lib().slat_host_free(self.ptr)
+        except Exception:
+            pass
+
+
+def pinned_empty(n: int, dtype) -> np.ndarray:
+    """An uninitialised numpy array of n elements in page-locked host memory."""
+    dt = np.dtype(dtype)
+    return np.asarray(_PinnedBuf(n * dt.itemsize))[:n * dt.itemsize].view(dt)
+
+
+def spgemm_host(a: HostCsr, b: HostCsr, ctx: Context | None = None, alloc=np.empty, flags: int = 0) -> HostCsr:
+    """C = A * B with host operands and a host result: the cost a drop-in pays for the reference's
+    signature (CsrMatrix::matmul(&self, &Self) -> Self over Vecs): both operands cross to the device,
+    the product runs, C comes back into host arrays from `alloc(n, dtype)` (np.empty: pageable;
+    pinned_empty: page-locked), and the device result is freed."""
+    ctx = ctx or default_context()
+    if a.dtype != b.dtype:
+        raise TypeError("operands must have the same value type")
+    va, vb = a.view(), b.view()
+    out = L.CsrOwned()
+    L.check(L.lib().slat_spgemm(ctx.ptr, C.byref(va), C.byref(vb), C.byref(out), flags), ctx.ptr)
+    try:
+        n, z = int(out.n_rows), int(out.nnz)
+        rp = alloc(n + 1, np.uint64)
+        col = alloc(max(z, 1), np.uint32)
+        val = alloc(max(z, 1), _VDT[a.dtype])
+        v = L.lib().slat_csr_view_of(C.byref(out))
+        L.check(L.lib().slat_csr_to_host(ctx.ptr, C.byref(v), rp.ctypes.data, col.ctypes.data, val.ctypes.data), ctx.ptr)
+    finally:
+        L.lib().slat_csr_free(ctx.ptr, C.byref(out))
+    return HostCsr(n, rp, col[:z], val[:z], a.dtype)
+
+
+# ------------------------------------------------------------------------------------------------
 # device-resident matrices
 # ------------------------------------------------------------------------------------------------
 class DeviceCsr:
