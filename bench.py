@@ -160,15 +160,19 @@ def golden(side: int, power: int):
 
 def parity(C, side: int, power: int):
     """C's row_ptr / col_idx / values SHA-256 against the golden digests (u32 values)."""
+    h = C.host()
+    return parity_arrays(h.row_ptr, h.col_idx, h.values, side, power)
+
+
+def parity_arrays(row_ptr, col_idx, values, side: int, power: int):
     import hashlib
     want = golden(side, power)
     if want is None:
         return None
-    h = C.host()
-    got = {"row_ptr": hashlib.sha256(np.asarray(h.row_ptr, dtype="<u8").tobytes()).hexdigest(),
-           "col": hashlib.sha256(np.asarray(h.col_idx, dtype="<u4").tobytes()).hexdigest(),
-           "val": hashlib.sha256(np.asarray(h.values, dtype="<u4").tobytes()).hexdigest()}
-    return int(C.nnz()) == want["nnz"] and all(got[k] == want[k] for k in got)
+    got = {"row_ptr": hashlib.sha256(np.asarray(row_ptr, dtype="<u8").tobytes()).hexdigest(),
+           "col": hashlib.sha256(np.asarray(col_idx, dtype="<u4").tobytes()).hexdigest(),
+           "val": hashlib.sha256(np.asarray(values, dtype="<u4").tobytes()).hexdigest()}
+    return len(col_idx) == want["nnz"] and all(got[k] == want[k] for k in got)
 
 
 def timed_steps(run, steps, warmup, barrier):
@@ -235,6 +239,16 @@ def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
         if rank == 0:
             par = parity(full, side, power)
         del full, C
+    elif dist is not None:
+        # gloo rehearsal (ranks sharing a GPU, no RCCL): the blocks assembled on the host
+        # (slat.dist.gather_blocks, the allgatherv restated over torch.distributed) and checked on rank 0
+        C = P.matmul_rowblock(lo, hi, A, 0)
+        h = C.host()
+        del C
+        rp, col, val = slat_dist.gather_blocks(h.row_ptr, h.col_idx, h.values)
+        if rank == 0:
+            par = parity_arrays(rp, col, val, side, power)
+        del rp, col, val, h
     elif world == 1:
         C = P.matmul_rowblock(0, n, A, 0)
         par = parity(C, side, power)

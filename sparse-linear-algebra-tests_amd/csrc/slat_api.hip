@@ -684,12 +684,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // Wide launches (columns beyond one window) split the rows by MAGNUS-style category into two
     // launches per pass: short rows in a per-wave LDS hash table (mode 1), the rest by row-span
     // windows (mode 2; numeric windows of 1024 words keep two blocks per CU).
-    static const bool kNoHash = slat_ab_knob("SLAT_NO_HASH") != nullptr;
-    const bool hash = asym.wide && !kNoHash;
-    if (hash) {
-        a.ww = std::min<uint32_t>(a.ww, 1024);
-        a.b_maxrow = asym.b_maxrow = (uint32_t)std::min<uint64_t>(maxrow_b, 0xFFFFFFFFull);
-    }
     // padded ELL copy of B when its rows are short (bounded blow-up)
     const uint64_t wq = (maxrow_b + 3) / 4;
     const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
@@ -708,6 +702,36 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
                      !kNoEll && !tiny;  // 24-bit row index, 31-bit byte offsets in the kernels
+    // stored bitmaps (single-window launches): symbolic keeps each row's touched bitmap blocks for
+    // numeric, n * ww words at most (only touched blocks are written), capped against free memory
+    // free device memory: re-read when this context's pool grew or shrank, else every 1024 calls
+    // (the query costs tens of microseconds of host time)
+    if (ctx->mem_changed || ctx->free_age++ % 1024 == 0) {
+        size_t total_b = 0;
+        (void)hipMemGetInfo(&ctx->free_b, &total_b);
+        ctx->mem_changed = false;
+    }
+    const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
+    static const bool kNoSbm = slat_ab_knob("SLAT_NO_SBM") != nullptr;
+    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny;
+    // a workgroup per row (slat_group.hip): single-window launches with B in ELL form. Symbolic for
+    // every value type; numeric for the semirings that add with atomics (f64 in the reference's fold
+    // order keeps the ordered wave-per-row walk), reading symbolic's stored bitmaps
+    static const bool kNoGroup = slat_ab_knob("SLAT_NO_GROUP") != nullptr;
+    const bool gsym = !a.wide && ell && !tiny && !kNoGroup && !ablate;
+    const bool gnum = gsym && sbm && (dt != SLAT_F64 || f64any);
+    static const bool kNoHash = slat_ab_knob("SLAT_NO_HASH") != nullptr;
+    // single-window launches (the 30^3 chain, configs C1 / C2 / C3) batch their short rows the same way
+    // (MAGNUS's small-row category) when the workgroup kernels take the rest: rows of <= 256 products
+    // (a bound: 4 per ELL group) in symbolic, <= 256 outputs in numeric, so every row numeric lists
+    // has a stored bitmap. f64 in the fold order keeps one kernel for every row
+    static const bool kNoShort1 = slat_ab_knob("SLAT_NO_SHORT1") != nullptr;
+    const bool short1 = gnum && !kNoShort1;
+    const bool hash = (asym.wide || short1) && !kNoHash;
+    if (hash) {
+        if (asym.wide) a.ww = std::min<uint32_t>(a.ww, 1024);
+        a.b_maxrow = asym.b_maxrow = (uint32_t)std::min<uint64_t>(maxrow_b, 0xFFFFFFFFull);
+    }
 
     // LDS sizing and grids. The numeric grid is the kernel's resident capacity (waves stride over
     // rows; measured faster than oversubscribing); symbolic takes up to 16 blocks per CU.
@@ -729,6 +753,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         uint32_t cb = 1;
         while (cb < 64 && ((ncols - 1) >> cb)) ++cb;
         a.cbits = cb <= 25 ? cb : 0;
+        if (!asym.wide) a.sym_cap = asym.sym_cap = kHashT / 2;  // every counted row fits numeric's table
     }
     const size_t hash_lds =
         (size_t)wpb * (dt == SLAT_U32     ? (!batched ? hash_bytes<SemU32>() : short_bytes<SemU32>())
@@ -769,18 +794,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const size_t shards_b = 4096 + (SLAT_PHASES ? 8192 : 0);  // + phase-timing slots (diagnostic builds)
     const size_t ecol_b = ell ? up256(B->n_rows * wq * 16) : 0, eval_b = ell ? up256(B->n_rows * wq * 4 * vs) : 0;
     const size_t eng_b = ell ? up256(B->n_rows) : 0;
-    // stored bitmaps (single-window launches): symbolic keeps each row's touched bitmap blocks for
-    // numeric, n * ww words at most (only touched blocks are written), capped against free memory
-    // free device memory: re-read when this context's pool grew or shrank, else every 1024 calls
-    // (the query costs tens of microseconds of host time)
-    if (ctx->mem_changed || ctx->free_age++ % 1024 == 0) {
-        size_t total_b = 0;
-        (void)hipMemGetInfo(&ctx->free_b, &total_b);
-        ctx->mem_changed = false;
-    }
-    const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
-    static const bool kNoSbm = slat_ab_knob("SLAT_NO_SBM") != nullptr;
-    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny;
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
@@ -795,7 +808,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
-    const size_t o_bmax = o_fat + fat_b, bmax_b = up256((size_t)sym_grid.x * 4);  // per-block max counts
+    const size_t o_bmax = o_fat + fat_b,  // per-block max counts (the group kernels' grid: <= 8 blocks per CU)
+        bmax_b = up256((size_t)std::max<uint64_t>(sym_grid.x, (uint64_t)ctx->cu_count * 8) * 4);
     if ((st = slat_ensure_ws(ctx, o_bmax + bmax_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (ell) {
@@ -974,6 +988,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         return e ? (uint32_t)std::atoi(e) : 2u;
     }();
     unsigned long long *tq = ctx->d_words + 5;
+    uint32_t sym_blocks = sym_grid.x;  // blocks of the symbolic launch whose maxima the scan reduces
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[0], s));
     if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return failc(st);
     if (sym_batched) {
@@ -988,7 +1003,13 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kWave - 1) / kWave / wpb + 1, ctx->cu_count * 16ull)));
         SLAT_HIPC(slat_launch_symbolic_short(idx32, g1, wpb * sym_short_bytes(), s, h1));
         h2.tq = (kDyn & 2u) ? tq : nullptr;
-        SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
+        if (asym.wide) {
+            SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
+        } else {  // the listed rows by the workgroup kernel (stored bitmaps for numeric)
+            const size_t glds = (size_t)asym.ww * 4;
+            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(sem, false, idx32, glds);
+            SLAT_HIPC(slat_launch_group_symbolic(idx32, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb))), glds, s, h2));
+        }
         a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
         a.list_cnt = lc + 16;
     } else if (hash) {
@@ -999,8 +1020,17 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     } else {
         // single-window launch without fat rows: symbolic leaves per-block max row counts for the
         // scan's last tile (<= 16 per scan thread)
-        if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
-        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
+        if (gsym) {
+            const size_t glds = (size_t)asym.ww * 4;
+            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(sem, false, idx32, glds);
+            const dim3 gg((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb)));
+            if (!fat && gg.x <= 16u * kScanThreads && gg.x * 4 <= bmax_b) asym.bmax = (uint32_t *)(ws + o_bmax);
+            SLAT_HIPC(slat_launch_group_symbolic(idx32, gg, glds, s, asym));
+            sym_blocks = gg.x;
+        } else {
+            if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
+            SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
+        }
     }
     hc.mark(5);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
@@ -1008,7 +1038,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const bool bpart = ell && dt != SLAT_F64;
     if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
                                bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
-                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch, asym.bmax, sym_grid.x)))
+                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch, asym.bmax, sym_blocks)))
         return failc(st);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
 
@@ -1026,7 +1056,18 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.c_col = C->col_idx;
     a.c_val = C->values;
     const int win_mode = hash ? 2 : 0;  // numeric instance of the window rows
-    auto launch_num = [&](const Args &x) { return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x); };
+    auto launch_num = [&](const Args &x) {
+        if (gnum && !a.wide) {
+            // a workgroup per row: ~12 KB of rank slots (2048 narrow outputs in one chunk)
+            Args g = x;
+            g.area = 12288;
+            const size_t glds = slat_group_numeric_lds(g.ww, g.area);
+            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(sem, true, idx32, glds);
+            const dim3 gg((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb)));
+            return slat_launch_group_numeric(sem, idx32, gg, glds, s, g);
+        }
+        return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x);
+    };
     if (ablate & ~7u) {
         // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
         // the real numeric pass below overwrites everything it wrote

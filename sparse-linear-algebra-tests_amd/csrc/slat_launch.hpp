@@ -3,6 +3,8 @@
 // and the symbolic ones in slat_sym.hip, so the library's kernels build in parallel.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
 
 namespace slat {
 struct Args;
@@ -56,3 +58,12 @@ hipError_t slat_launch_tiny(int sem, dim3 grid, size_t lds, hipStream_t s, const
                             unsigned long long *status, uint32_t epoch, unsigned long long *maxw);
 // the batched short-row symbolic of wide launches (lists the other rows for mode 2)
 hipError_t slat_launch_symbolic_short(bool idx32, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
+
+// a workgroup per row (slat_group.hip): single-window launches with B in ELL form. Symbolic for every
+// value type (it reads no values); numeric for u32, Sat64 and f64 in any order (sem ids above)
+hipError_t slat_launch_group_symbolic(bool idx32, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
+hipError_t slat_launch_group_numeric(int sem, bool idx32, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
+// the numeric instance's dynamic LDS for a window of ww words and `area` bytes of rank slots
+size_t slat_group_numeric_lds(uint32_t ww, uint32_t area);
+// resident 256-thread blocks per CU of the symbolic (numeric = false) or numeric instance at `lds`
+int slat_group_blocks_per_cu(int sem, bool numeric, bool idx32, size_t lds);

@@ -144,6 +144,10 @@ struct Args {
     // walks only its chunks' part of each B row instead of the whole row with a column filter
     const uint32_t *wsplit;
     uint32_t wnch1;
+    // k_symbolic_short: a batch's product bound (0: kSymHashT * SLAT_SYM_CAP_PCT %). Single-window
+    // launches take kHashT / 2, so every row it counts fits k_numeric_short's table and every row it
+    // lists (the workgroup kernels') gets a stored bitmap
+    uint32_t sym_cap;
 };
 
 __device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.fr_mark && p.fr_mark[row]; }
@@ -2067,7 +2071,7 @@ __host__ __device__ constexpr uint32_t sym_short_bytes() { return kSymHashT * 4 
 template <typename I>
 __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
     constexpr int kWpb = kBlock / kWave;
-    constexpr uint32_t kCap = kSymHashT * SLAT_SYM_CAP_PCT / 100;
+    const uint32_t kCap = p.sym_cap ? p.sym_cap : kSymHashT * SLAT_SYM_CAP_PCT / 100;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
