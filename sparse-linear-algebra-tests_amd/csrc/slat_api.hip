@@ -717,7 +717,18 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // a workgroup per row (slat_group.hip): single-window launches with B in ELL form. Symbolic for
     // every value type; numeric for the semirings that add with atomics (f64 in the reference's fold
     // order keeps the ordered wave-per-row walk), reading symbolic's stored bitmaps
-    static const bool kNoGroup = slat_ab_knob("SLAT_NO_GROUP") != nullptr;
+    // (SLAT_GROUP=1: the workgroup-per-row kernels for the long rows instead of the wave-per-row ones;
+    // measured slower on the 30^3 chain)
+    static const bool kNoGroup = slat_ab_knob("SLAT_GROUP") == nullptr;
+    // threads per row of the group kernels (A/B knobs SLAT_GRP_SYM_T / SLAT_GRP_NUM_T: 128 or 256)
+    static const int kGrpSymT = [] {
+        const char *e = slat_ab_knob("SLAT_GRP_SYM_T");
+        return e && std::atoi(e) == 256 ? 256 : 128;
+    }();
+    static const int kGrpNumT = [] {
+        const char *e = slat_ab_knob("SLAT_GRP_NUM_T");
+        return e && std::atoi(e) == 128 ? 128 : 256;
+    }();
     const bool gsym = !a.wide && ell && !tiny && !kNoGroup && !ablate;
     const bool gnum = gsym && sbm && (dt != SLAT_F64 || f64any);
     static const bool kNoHash = slat_ab_knob("SLAT_NO_HASH") != nullptr;
@@ -726,7 +737,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // (a bound: 4 per ELL group) in symbolic, <= 256 outputs in numeric, so every row numeric lists
     // has a stored bitmap. f64 in the fold order keeps one kernel for every row
     static const bool kNoShort1 = slat_ab_knob("SLAT_NO_SHORT1") != nullptr;
-    const bool short1 = gnum && !kNoShort1;
+    const bool short1 = !a.wide && ell && !tiny && !ablate && (dt != SLAT_F64 || f64any) && !kNoShort1;
     const bool hash = (asym.wide || short1) && !kNoHash;
     if (hash) {
         if (asym.wide) a.ww = std::min<uint32_t>(a.ww, 1024);
@@ -753,10 +764,22 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         uint32_t cb = 1;
         while (cb < 64 && ((ncols - 1) >> cb)) ++cb;
         a.cbits = cb <= 25 ? cb : 0;
-        if (!asym.wide) a.sym_cap = asym.sym_cap = kHashT / 2;  // every counted row fits numeric's table
+        if (!asym.wide) {
+            a.sym_cap = asym.sym_cap = kHashT / 2;  // every counted row fits numeric's table
+            // tiles of fewer rows when 64-row tiles would leave most resident waves idle (27 000 rows:
+            // 422 tiles for ~6 000 waves): about 4 tiles per CU slot of 16 waves
+            const uint64_t t = (n + (uint64_t)ctx->cu_count * 16 - 1) / ((uint64_t)ctx->cu_count * 16);
+            a.tile_rows = asym.tile_rows = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, t));
+        }
     }
+    // every row short (single-window launches): A's longest row x B's longest row rounded up to ELL
+    // groups (k_symbolic_short's bound, 4 per group) fits the short tables, so the symbolic pass lists
+    // no row and the window launches are skipped; numeric's short launch stores the completion word
+    // (C1: A^2 of the 30^3 torus, 7 x 8 = 56 products a row)
+    const bool all_short = sym_batched && batched && !asym.wide && A->max_row_nnz &&
+                           (unsigned __int128)A->max_row_nnz * (4 * ((maxrow_b + 3) / 4)) <= kHashT / 2;
     const size_t hash_lds =
-        (size_t)wpb * (dt == SLAT_U32     ? (!batched ? hash_bytes<SemU32>() : short_bytes<SemU32>())
+        (size_t)wpb * (dt == SLAT_U32    ? (!batched ? hash_bytes<SemU32>() : short_bytes<SemU32>())
                        : dt == SLAT_SAT64 ? (!batched ? hash_bytes<SemSat64>() : short_bytes<SemSat64>())
                        : f64any ? (!batched ? hash_bytes<SemF64Any>() : short_bytes<SemF64Any>())
                                 : hash_bytes<SemF64>());
@@ -1000,15 +1023,18 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         h1.cbits = a.cbits;
         h1.list = h2.list = (uint32_t *)(ws + o_l1);
         h1.list_cnt = h2.list_cnt = lc;
-        const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + kWave - 1) / kWave / wpb + 1, ctx->cu_count * 16ull)));
+        const uint64_t trows = h1.tile_rows ? h1.tile_rows : kWave;
+        const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + trows - 1) / trows / wpb + 1, ctx->cu_count * 16ull)));
         SLAT_HIPC(slat_launch_symbolic_short(idx32, g1, wpb * sym_short_bytes(), s, h1));
-        h2.tq = (kDyn & 2u) ? tq : nullptr;
-        if (asym.wide) {
+        h2.tq = (kDyn & 2u) && asym.wide ? tq : nullptr;  // (single-window rows: a fixed stride)
+        if (all_short) {
+            // (no listed rows)
+        } else if (asym.wide || !gsym) {
             SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
         } else {  // the listed rows by the workgroup kernel (stored bitmaps for numeric)
             const size_t glds = (size_t)asym.ww * 4;
-            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(sem, false, idx32, glds);
-            SLAT_HIPC(slat_launch_group_symbolic(idx32, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb))), glds, s, h2));
+            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(kGrpSymT, sem, false, idx32, glds, asym.ww);
+            SLAT_HIPC(slat_launch_group_symbolic(kGrpSymT, idx32, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb))), glds, s, h2));
         }
         a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
         a.list_cnt = lc + 16;
@@ -1022,10 +1048,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         // scan's last tile (<= 16 per scan thread)
         if (gsym) {
             const size_t glds = (size_t)asym.ww * 4;
-            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(sem, false, idx32, glds);
+            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(kGrpSymT, sem, false, idx32, glds, asym.ww);
             const dim3 gg((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb)));
             if (!fat && gg.x <= 16u * kScanThreads && gg.x * 4 <= bmax_b) asym.bmax = (uint32_t *)(ws + o_bmax);
-            SLAT_HIPC(slat_launch_group_symbolic(idx32, gg, glds, s, asym));
+            SLAT_HIPC(slat_launch_group_symbolic(kGrpSymT, idx32, gg, glds, s, asym));
             sym_blocks = gg.x;
         } else {
             if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
@@ -1062,9 +1088,9 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             Args g = x;
             g.area = 12288;
             const size_t glds = slat_group_numeric_lds(g.ww, g.area);
-            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(sem, true, idx32, glds);
+            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(kGrpNumT, sem, true, idx32, glds, g.ww);
             const dim3 gg((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb)));
-            return slat_launch_group_numeric(sem, idx32, gg, glds, s, g);
+            return slat_launch_group_numeric(kGrpNumT, sem, idx32, gg, glds, s, g);
         }
         return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x);
     };
@@ -1078,21 +1104,26 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIPC(launch_num(abl));
         SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
     }
+    // the call's last kernel stores the completion word itself unless fat rows or the stats copy
+    // follow (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
+    static const bool kFusedSignal = slat_ab_knob("SLAT_NO_FUSED_SIGNAL") == nullptr;
+    const bool fused = kFusedSignal && !fat && !a.stats && wait_mode() == 0;
     if (hash) {
         Args h1 = a;
         if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
         h1.tq = (kDyn & 2u) && hash_mode != 3 ? tq : nullptr;
+        if (all_short && fused) {
+            a.seq = h1.seq = ++ctx->done_seq;
+            h1.done = ctx->d_words + 6;
+        }
         SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
     }
-    a.tq = (kDyn & 2u) && hash ? tq : nullptr;
-    // the window pass is the call's last kernel unless fat rows or the stats copy follow: it stores
-    // the completion word itself (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
-    static const bool kFusedSignal = slat_ab_knob("SLAT_NO_FUSED_SIGNAL") == nullptr;
-    if (kFusedSignal && !fat && !a.stats && wait_mode() == 0) {
+    a.tq = (kDyn & 2u) && hash && a.wide ? tq : nullptr;  // (single-window rows: a fixed stride)
+    if (fused && !all_short) {
         a.seq = ++ctx->done_seq;
         a.done = ctx->d_words + 6;
     }
-    SLAT_HIPC(launch_num(a));
+    if (!all_short) SLAT_HIPC(launch_num(a));
     if (wsplit) slat_dev_free(ctx, wsplit, s);  // stream-ordered: reused only by later work
     if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return failc(st);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));

@@ -148,6 +148,9 @@ struct Args {
     // launches take kHashT / 2, so every row it counts fits k_numeric_short's table and every row it
     // lists (the workgroup kernels') gets a stored bitmap
     uint32_t sym_cap;
+    // k_symbolic_short / k_numeric_short: rows per wave tile (0: 64). Fewer when the launch has too
+    // few rows to give every resident wave a 64-row tile (the 30^3 chain's 27 000 rows: 422 tiles)
+    uint32_t tile_rows;
 };
 
 __device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.fr_mark && p.fr_mark[row]; }
@@ -2026,10 +2029,12 @@ __device__ __forceinline__ void stage_groups(uint32_t base, uint32_t mxg, const 
 // prefix of the entries' group counts, read at each row's first and end entry (mod 2^32: only rows
 // of <= 256 entries use the difference, and the entries of longer rows are skipped, not read).
 // pf: u32[256] of LDS, left dirty.
-__device__ __forceinline__ uint32_t tile_groups(const Args &p, uint64_t A0j, uint64_t A1j, uint32_t nt, uint32_t *pf) {
+// Rows of more than `jump` entries are jumped over (their bound is never needed: they are long).
+__device__ __forceinline__ uint32_t tile_groups(const Args &p, uint64_t A0j, uint64_t A1j, uint32_t nt, uint32_t *pf,
+                                                uint64_t jump = 256) {
     const uint32_t lane = (uint32_t)lane_id();
     const uint64_t T0 = readlane_u64(A0j, 0), T1 = readlane_u64(A1j, (int)nt - 1);
-    const bool longj = lane < nt && A1j - A0j > 256;
+    const bool longj = lane < nt && A1j - A0j > jump;
     uint32_t gs = 0, ge = 0, run = 0;
     for (uint64_t c0 = T0; c0 < T1;) {
         const unsigned long long in = __ballot(longj && A0j <= c0 && c0 < A1j);
@@ -2091,24 +2096,29 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
     wave_sync();
     const uint32_t cb = p.cbits;
     unsigned long long flops = 0;
-    const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
+    const uint32_t T = p.tile_rows ? p.tile_rows : (uint32_t)kWave;
+    const uint64_t ntiles = (p.nrows + T - 1) / T;
     const XcdStride xs(ntiles, kWpb, wv);
     for (uint64_t tile = xs.first; tile < xs.end; tile += xs.stride) {
-        const uint64_t r0 = tile * kWave, r = r0 + lane;
-        const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
+        const uint64_t r0 = tile * T, r = r0 + lane;
+        const uint32_t nt = (uint32_t)min<uint64_t>(T, p.nrows - r0);
         uint64_t A0j = 0, A1j = 0;
         if ((uint32_t)lane < nt) {
             A0j = p.a_rp[r];
             A1j = p.a_rp[r + 1];
         }
         const uint64_t lj = A1j - A0j;
-        // product bound: 4 per ELL group (the markers serve as the prefix window, then are cleared)
-        const uint32_t gj = tile_groups(p, A0j, A1j, nt, marks);
+        // product bound: 4 per ELL group (the markers serve as the prefix window, then are cleared).
+        // With a small cap (single-window launches) a row of more than cap / 4 entries is taken as
+        // long without reading its entries (bound >= 4 per entry with a non-empty B row; a row sent
+        // long with empty B rows among its entries is still correct, only another category)
+        const uint64_t jump = p.sym_cap ? (uint64_t)kCap / 4 : 256;
+        const uint32_t gj = tile_groups(p, A0j, A1j, nt, marks, jump);
         const uint32_t bj = gj > 0x3FFFFFFFu ? 0xFFFFFFFFu : 4 * gj;
         ((uint4 *)marks)[lane] = make_uint4(0, 0, 0, 0);
         wave_sync();
         const bool fatj = (uint32_t)lane < nt && fat_row(p, r);
-        const bool shortj = (uint32_t)lane < nt && bj <= kCap && lj <= 256 && !fatj;
+        const bool shortj = (uint32_t)lane < nt && bj <= kCap && lj <= jump && !fatj;
         const unsigned long long shortm = __ballot(shortj);
         list_rows(p, (uint32_t)lane < nt && !shortj && !fatj, r);
         uint32_t b = 0;
@@ -2413,13 +2423,14 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
     // packed emit keys (batch_emit PACK): batches of <= 8 rows whose composite keys, shifted past a
     // 9-bit slot, stay below kSent
     const bool pack = SLAT_SHORT_PACK && cb > 0 && cb <= 20 && ((((7ull << cb) | (p.ncols - 1)) << 9) | 511ull) < 0xFFFFFFFFull;
-    const uint64_t ntiles = (p.nrows + kWave - 1) / kWave;
+    const uint32_t T = p.tile_rows ? p.tile_rows : (uint32_t)kWave;
+    const uint64_t ntiles = (p.nrows + T - 1) / T;
     PhaseClock pc{};  // diagnostic builds (SLAT_PHASES): where the waves' time goes
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
     const XcdStride xs(ntiles, kWpb, wv);
     for (uint64_t tile = xs.first; tile < xs.end; tile += xs.stride) {
-        const uint64_t r0 = tile * kWave, r = r0 + lane;
-        const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
+        const uint64_t r0 = tile * T, r = r0 + lane;
+        const uint32_t nt = (uint32_t)min<uint64_t>(T, p.nrows - r0);
         uint64_t A0j = 0, A1j = 0, obj = 0, oej = 0;
         if ((uint32_t)lane < nt) {
             A0j = p.a_rp[r];

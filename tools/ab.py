@@ -19,7 +19,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(c4: bool, steps: int, only_c4: bool = False, sat64: bool = False):
+def child(c4: bool, steps: int, only_c4: bool = False, sat64: bool = False, chain: bool = False):
     sys.path.insert(0, os.path.join(ROOT, "sparse-linear-algebra-tests_amd"))
     import numpy as np
 
@@ -28,6 +28,8 @@ def child(c4: bool, steps: int, only_c4: bool = False, sat64: bool = False):
     out = {}
     legs = ([] if only_c4 else [("a7", 30, 7, steps)]) + ([("c4", 100, 4, max(10, steps // 10))] if c4 or only_c4 else [])
     legs += [("s7", 30, 7, steps)] if sat64 else []
+    # the 30^3 chain's other steps A^(k-1) * A (C1 = a2): the fixed cost per call and per row
+    legs += [(f"a{k}", 30, k, steps) for k in range(2, 7)] if chain else []
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
     for name, side, power, k in legs:
         A = slat.torus_thinned_device(side, 3.0, slat.StdRng(), ctx)
@@ -67,10 +69,11 @@ def main():
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--only-c4", action="store_true", help="child: the C4 leg alone")
     ap.add_argument("--sat64", action="store_true", help="add the Sat64 (MagnusMatrix) A^6*A leg")
+    ap.add_argument("--chain", action="store_true", help="add the 30^3 chain's A^2 ... A^6 legs")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     if a.child:
-        child(a.c4, a.steps, a.only_c4, a.sat64)
+        child(a.c4, a.steps, a.only_c4, a.sat64, a.chain)
         return
     res = {}
     for r in range(a.reps):
@@ -85,7 +88,7 @@ def main():
                 k, _, val = kv.partition("=")
                 env[k] = val
             cmd = ([sys.executable, os.path.abspath(__file__), "--child", "--steps", str(a.steps)] + (["--c4"] if a.c4 else [])
-                   + (["--sat64"] if a.sat64 else []))
+                   + (["--sat64"] if a.sat64 else []) + (["--chain"] if a.chain else []))
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
                 print(f"{v}: FAILED rc={p.returncode}\n{p.stderr[-3000:]}", flush=True)
