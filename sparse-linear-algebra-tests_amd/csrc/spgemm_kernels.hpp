@@ -1523,13 +1523,16 @@ void k_symbolic(Args p) {
         if (threadIdx.x == 0) s_bmax = s_bdone = 0;
         __syncthreads();
     }
+    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
+    const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
+    // a wave with no listed row leaves before touching LDS (C4 lists none: the launch is then
+    // only its dispatch)
+    if (listed && !p.bmax && (uint64_t)blockIdx.x * kWpb + wv >= nit) return;
     for (uint32_t w = lane; w < region_w; w += kWave) L0[w] = MODE == 1 ? kSent : 0u;
     wave_sync();
     unsigned long long flops = 0;
     uint64_t mx = 0;  // max row count (p.bmax)
     const uint64_t stride = (uint64_t)gridDim.x * kWpb;
-    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
-    const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     // tickets only in the wide launches' passes (MODE 1 / 2): the code costs the single-window
     // instance 18 VGPRs even unused
     const bool dyn = MODE != 0 && p.tq != nullptr;  // launch-uniform
@@ -1576,6 +1579,10 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
     constexpr bool kVals = !Sem::kOrdered;  // f64 accumulates from an ordered CSR walk
 
     const int lane = lane_id();
+    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
+    const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
+    // a wave with no listed row leaves before touching LDS (C4 lists none)
+    if (listed && first >= nit) return;
     const NumLayout lay = num_layout(p.ww, p.area);
     // per-wave region: the bitmap window + rank slots, or (wide launches) the hash table in the
     // same place
@@ -1622,8 +1629,6 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
     if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
     auto mark = [&](int i) { pc.mark(i); };
     uint64_t *ph = pc.ph;
-    const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
-    const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
     using RW = RowWalker<Sem, I, ELL, kVals>;
     const bool dyn = MODE != 0 && p.tq != nullptr;  // launch-uniform (single-window passes: a fixed stride)
     const TicketQueue tq(p.tq, nit, stride);

@@ -182,6 +182,8 @@ def lib():
         "slat_host_free": ([vp], C.c_int),
     }
     for name, (args, res) in sig.items():
+        if os.environ.get("SLAT_LIB_PATH") and not hasattr(L, name):
+            continue  # an older variant build (A/B against a previous round's library)
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
