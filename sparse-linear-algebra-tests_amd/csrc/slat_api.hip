@@ -776,7 +776,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // groups (k_symbolic_short's bound, 4 per group) fits the short tables, so the symbolic pass lists
     // no row and the window launches are skipped; numeric's short launch stores the completion word
     // (C1: A^2 of the 30^3 torus, 7 x 8 = 56 products a row)
-    const bool all_short = sym_batched && batched && !asym.wide && A->max_row_nnz &&
+    // (maxrow_b > 0: with an empty B the bound says nothing about a row's entry count)
+    const bool all_short = sym_batched && batched && !asym.wide && A->max_row_nnz && maxrow_b > 0 &&
                            (unsigned __int128)A->max_row_nnz * (4 * ((maxrow_b + 3) / 4)) <= kHashT / 2;
     const size_t hash_lds =
         (size_t)wpb * (dt == SLAT_U32    ? (!batched ? hash_bytes<SemU32>() : short_bytes<SemU32>())
@@ -1017,11 +1018,12 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     if (sym_batched) {
         // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
         // row's products per tile, listing the rest), then the listed rows by windows
-        unsigned int *lc = (unsigned int *)(ws + o_lc);
-        SLAT_HIPC(hipMemsetAsync(lc, 0, lc_b, s));
+        // (every row short: no lists, so no counters to clear)
+        unsigned int *lc = all_short ? nullptr : (unsigned int *)(ws + o_lc);
+        if (lc) SLAT_HIPC(hipMemsetAsync(lc, 0, lc_b, s));
         Args h1 = asym, h2 = asym;
         h1.cbits = a.cbits;
-        h1.list = h2.list = (uint32_t *)(ws + o_l1);
+        h1.list = h2.list = all_short ? nullptr : (uint32_t *)(ws + o_l1);
         h1.list_cnt = h2.list_cnt = lc;
         const uint64_t trows = h1.tile_rows ? h1.tile_rows : kWave;
         const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + trows - 1) / trows / wpb + 1, ctx->cu_count * 16ull)));
@@ -1036,8 +1038,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(kGrpSymT, sem, false, idx32, glds, asym.ww);
             SLAT_HIPC(slat_launch_group_symbolic(kGrpSymT, idx32, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb))), glds, s, h2));
         }
-        a.list = (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
-        a.list_cnt = lc + 16;
+        a.list = all_short ? nullptr : (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
+        a.list_cnt = all_short ? nullptr : lc + 16;
     } else if (hash) {
         Args h1 = asym;
         h1.tq = (kDyn & 2u) ? tq : nullptr;

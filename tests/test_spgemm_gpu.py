@@ -411,3 +411,35 @@ def test_sat64_narrow_bound_clamped_a_values(ctx, b_form, n):
     for flags in (0, slat.FLAG_NO_TINY):
         got = to_dev(a, slat.SAT64)._spgemm(to_dev(b, slat.SAT64), flags)
         assert_same(got, O.matmul_seq(a, b), f"Sat64 clamped A max, B {b_form}, n={n}, flags={flags}")
+
+
+@pytest.mark.parametrize("case", ["all_short", "mixed", "empty_b", "zeros"])
+@pytest.mark.parametrize("dtype", [slat.U32, slat.SAT64])
+def test_single_window_short_row_categories(ctx, case, dtype):
+    """Single-window launches (columns within one LDS window, > 2048 rows: not the one-kernel path)
+    batch their short rows in hash tables. all_short: max row of A x max row of B rounded up to ELL
+    groups <= 256, so no row is listed and only the short-row kernels run (the completion word is
+    stored by the numeric short launch); mixed: rows of 100 entries among short ones go to the
+    window kernels; empty_b: A rows of 300 entries against an empty B (nothing listed, every count
+    0); zeros: explicit zero values in B's short rows (the zero-row count of the short kernels)."""
+    rng = np.random.default_rng({"all_short": 1, "mixed": 2, "empty_b": 3, "zeros": 4}[case])
+    n = 5000
+    lens = rng.integers(0, 9, n)
+    if case == "mixed":
+        lens[::97] = 100
+    if case == "empty_b":
+        lens[::50] = 300
+    ar = np.repeat(np.arange(n), lens)
+    ac = np.concatenate([rng.choice(n, k, replace=False) for k in lens])
+    av = rng.integers(1, 1 << 20, len(ar))
+    a = O.from_coo(n, ar, ac, av, DT[dtype])
+    if case == "empty_b":
+        b = O.from_coo(n, [], [], [], DT[dtype])
+    else:
+        bl = rng.integers(1, 8, n)
+        br = np.repeat(np.arange(n), bl)
+        bc = np.concatenate([rng.choice(n, k, replace=False) for k in bl])
+        bv = rng.integers(0 if case == "zeros" else 1, 5, len(br))
+        b = O.from_coo(n, br, bc, bv, DT[dtype])
+    got = to_dev(a, dtype)._spgemm(to_dev(b, dtype))
+    assert_same(got, O.matmul_seq(a, b), f"single-window {case}")

@@ -13,3 +13,6 @@ tail -n 4 $OUT/heavy.txt | cut -c1-900
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 tools/ab.py --child --steps 20 --chain --c4 > $OUT/child.json 2> $OUT/child.err || { tail -20 $OUT/child.err; exit 1; }
 cat $OUT/child.json
 python3 tools/trace_table.py $OUT/trace > $OUT/trace_table.txt && head -30 $OUT/trace_table.txt
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/htrace -o run --output-format csv -- python3 tools/ab_heavy.py --child --legs rg,c5any,c5ord > $OUT/hchild.json 2> $OUT/hchild.err || { tail -20 $OUT/hchild.err; exit 1; }
+cat $OUT/hchild.json
+python3 tools/trace_table.py $OUT/htrace > $OUT/htrace_table.txt && head -25 $OUT/htrace_table.txt
