@@ -57,10 +57,16 @@ __host__ __device__ constexpr uint32_t fr_chunk() {
     return (fr_kb<Sem>() * 1024u) / (uint32_t)(sizeof(typename Sem::V) * Sem::kSlots);
 }
 constexpr uint32_t kMaxBuckets = 256;  // accumulator chunks a bucketed row may span (LDS counters)
+// LDS per wave of the flattened walk (fr_flat below): entry bases I[64] | A values S[64] (VALS) |
+// markers u8[256]
+template <typename S, bool VALS, typename I>
+__host__ __device__ constexpr uint32_t fr_flat_bytes() {
+    return kWave * (uint32_t)(sizeof(I) + (VALS ? sizeof(S) : 0)) + 4 * kWave;
+}
 template <typename Sem>
 __host__ __device__ constexpr size_t fr_lds() {
     return (size_t)fr_chunk<Sem>() * sizeof(typename Sem::V) * Sem::kSlots + fr_chunk<Sem>() / 8 + 64 * 8 +
-           (Sem::kOrdered ? 0 : 2 * kMaxBuckets * 4);
+           (Sem::kOrdered ? 0 : 2 * kMaxBuckets * 4 + kFW * fr_flat_bytes<typename Sem::S, true, uint64_t>());
 }
 
 __device__ __forceinline__ uint32_t cap63(uint64_t x) { return x < 63 ? (uint32_t)x : 63u; }
@@ -247,6 +253,91 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
     }
 }
 
+// The flattened walk (SLAT_FR_FLAT; variant builds -DSLAT_FR_FLAT=0 keep fr_walk): every product of A
+// row [a0, a1) by one block, wave w taking A entries w + 8 * lane, + 512, ... one per lane. The
+// entries' B parts [bs, bs + len) are laid end to end and walked 256 products per pass, four per
+// lane (product j = e*64 + lane of the pass: consecutive lanes on consecutive entries of a part), so
+// every lane is busy whatever the parts' lengths (a hub's long B row and many one-entry parts alike)
+// and a pass's loads are in flight together. fr_walk instead gives each lane its own entries and
+// the wave waits on the longest; with R-MAT's skewed part lengths most lanes sat idle. Lane -> entry
+// by markers: each part's first product in the pass marks its entry (lane + 1) and a running max
+// over the pass's positions spreads it. part(k, bs, len): entry k's B part. wl: the wave's LDS,
+// fr_flat_bytes<S, VALS, I>(): entry bases I[64] | A values S[64] (VALS) | markers u8[256].
+#ifndef SLAT_FR_FLAT
+#define SLAT_FR_FLAT 1
+#endif
+constexpr uint32_t kFlatHuge = 1u << 24;  // parts at least this long: walked by the whole wave alone
+template <typename S, bool VALS, typename I, typename Part, typename F>
+__device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, F &&fn, uint8_t *wl) {
+    const int lane = lane_id();
+    const int wv = threadIdx.x / kWave;
+    I *eb = (I *)wl;
+    S *ea = (S *)(wl + kWave * sizeof(I));
+    uint8_t *mk = wl + kWave * (sizeof(I) + (VALS ? sizeof(S) : 0));
+    const S *av = (const S *)p.a_val;
+    const S *bv = (const S *)p.b_val;
+    const auto plus = [](uint32_t x, uint32_t y) { return x + y; };
+    const auto mx = [](uint32_t x, uint32_t y) { return max(x, y); };
+    // wave w's entries: w, w + 8, w + 16, ... (a row of 100 entries keeps all 8 waves busy)
+    for (I base = a0 + (I)wv; base < a1; base += (I)kFB) {
+        const I i = base + (I)lane * (I)kFW;
+        I bs = 0;
+        uint32_t len = 0;
+        S a = S(0);
+        if (i < a1) {
+            const uint32_t k = p.a_col[i];
+            if constexpr (VALS) a = av[i];
+            if (k < p.b_nrows) part(k, bs, len);
+        }
+        // a part of 2^24 or more entries on its own (the flat offsets stay below 2^30)
+        for (unsigned long long m = __ballot(len >= kFlatHuge); m; m &= m - 1) {
+            const int l0 = (int)__builtin_ctzll(m);
+            const I s0 = (I)readlane_u64((uint64_t)bs, l0);
+            const I e0 = s0 + (I)readlane_u32(len, l0);
+            const S at = readlane_val(a, l0);
+            for (I j = s0 + (I)lane; j < e0; j += (I)kWave) fn(p.b_col[j], at, VALS ? bv[j] : S(0));
+        }
+        if (len >= kFlatHuge) len = 0;
+        const uint32_t incl = wave_incl_scan(len, 0u, plus);
+        const uint32_t tot = readlane_u32(incl, kWave - 1);
+        if (tot == 0) continue;  // wave-uniform
+        const uint32_t off = incl - len;
+        eb[lane] = bs - (I)off;  // product j of the entry: B index eb + j
+        if constexpr (VALS) ea[lane] = a;
+        for (uint32_t p0 = 0; p0 < tot; p0 += 4 * kWave) {
+            if (len && off < p0 + 4 * kWave && off + len > p0) mk[max(off, p0) - p0] = (uint8_t)(lane + 1);
+            wave_sync();
+            uint32_t L[4], carry = 0;
+            sfor<4>([&](auto E) {
+                const uint32_t m = mk[E * kWave + lane];
+                L[E] = max(wave_incl_scan(m, 0u, mx), carry);
+                carry = readlane_u32(L[E], kWave - 1);
+            });
+            sfor<4>([&](auto E) { mk[E * kWave + lane] = 0; });
+            uint32_t c[4];
+            S v[4], aa[4];
+            sfor<4>([&](auto E) {
+                const uint32_t j = p0 + E * kWave + (uint32_t)lane;
+                c[E] = kSent;
+                v[E] = aa[E] = S(0);
+                if (j < tot) {
+                    const uint32_t l = L[E] - 1;  // position 0 is always marked: L >= 1
+                    const I bi = eb[l] + (I)j;
+                    c[E] = p.b_col[bi];
+                    if constexpr (VALS) {
+                        v[E] = bv[bi];
+                        aa[E] = ea[l];
+                    }
+                }
+            });
+            sfor<4>([&](auto E) {
+                if (c[E] != kSent) fn(c[E], aa[E], v[E]);
+            });
+            wave_sync();  // the markers clear before the next pass writes them
+        }
+    }
+}
+
 // the split table of B by accumulator chunk (FatArgs::split): thread per (row k, boundary c), a
 // binary search in the sorted row; boundary 0 is 0 and boundary nch1 - 1 the row length
 __global__ __launch_bounds__(kBlock) void k_fr_splits(const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb,
@@ -301,6 +392,10 @@ __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
     extern __shared__ __attribute__((aligned(16))) uint32_t bits[];
     uint32_t *sh = bits + kWords;
     unsigned long long *shm = (unsigned long long *)(bits + kWords + kFW);
+    // the flattened walk's per-wave region (one pass over all columns), markers clear
+    constexpr uint32_t kFlat = fr_flat_bytes<uint32_t, false, I>();
+    uint8_t *wl = (uint8_t *)(shm + kFW) + (threadIdx.x / kWave) * kFlat;
+    ((uint32_t *)(wl + kFlat - 4 * kWave))[lane_id()] = 0;
     const unsigned int nl = *(volatile unsigned int *)f.cnt;
     for (uint32_t w = threadIdx.x; w < kWords; w += kFB) bits[w] = 0;
     __syncthreads();
@@ -314,10 +409,20 @@ __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
         for (uint64_t lo = 0; lo < p.ncols; lo += SB) {
             const uint32_t hi = (uint32_t)min<uint64_t>(p.ncols, lo + SB);
             const bool all = lo == 0 && hi == p.ncols;
-            fr_walk<uint32_t, false, I>(p, a0, a1, (uint32_t)lo, hi, all, [&](uint32_t c, uint32_t, uint32_t) {
+            auto mark = [&](uint32_t c, uint32_t, uint32_t) {
                 const uint32_t o = c - (uint32_t)lo;
                 atomicOr(&bits[o >> 5], 1u << (o & 31));
-            });
+            };
+            if (SLAT_FR_FLAT && all)
+                fr_flat<uint32_t, false, I>(
+                    p, a0, a1,
+                    [&](uint32_t k, I &bs, uint32_t &len) {
+                        bs = (I)p.b_rp[k];
+                        len = (uint32_t)min<uint64_t>((uint64_t)((I)p.b_rp[k + 1] - bs), 0xFFFFFFFFull);
+                    },
+                    mark, wl);
+            else
+                fr_walk<uint32_t, false, I>(p, a0, a1, (uint32_t)lo, hi, all, mark);
             __syncthreads();
             uint32_t pc = 0;
             for (uint32_t w = threadIdx.x; w < kWords; w += kFB) {
@@ -351,13 +456,32 @@ __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
 // walks the A entries in order, lanes over one B row (distinct columns): one writer per column.
 template <typename Sem, typename I>
 __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint32_t c0, uint32_t c1,
-                                              typename Sem::V *acc, uint32_t *bits) {
+                                              typename Sem::V *acc, uint32_t *bits, uint8_t *wl) {
     using S = typename Sem::S;
     const Args &p = f.a;
     const S *av = (const S *)p.a_val;
     const S *bv = (const S *)p.b_val;
     // the chunk's granules in the split table: [g0, g1)
     const uint32_t g0 = c0 >> f.gsh, g1 = min(f.nch1 - 1, (c1 + (1u << f.gsh) - 1) >> f.gsh);
+    if constexpr (!Sem::kOrdered && SLAT_FR_FLAT) {
+        if (f.split) {  // the chunk's part of each B row from the split table: no filtering
+            fr_flat<S, true, I>(
+                p, a0, a1,
+                [&](uint32_t k, I &bs, uint32_t &len) {
+                    const uint32_t *sp = f.split + (uint64_t)k * f.nch1;
+                    const uint32_t s0 = sp[g0];
+                    bs = (I)p.b_rp[k] + (I)s0;
+                    len = sp[g1] - s0;
+                },
+                [&](uint32_t c, S a, S b) {
+                    const uint32_t o = c - c0;
+                    Sem::acc(acc, o, Sem::prod(a, b));
+                    atomicOr(&bits[o >> 5], 1u << (o & 31));
+                },
+                wl);
+            return;
+        }
+    }
     if constexpr (!Sem::kOrdered) {
         const bool all = c0 == 0 && c1 == p.ncols;
         fr_walk<S, true, I>(p, a0, a1, c0, c1, all, [&](uint32_t c, S a, S b) {
@@ -528,6 +652,10 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
     uint32_t *bits = (uint32_t *)(smem + (size_t)CH * sizeof(V) * Sem::kSlots);
     uint32_t *sh = bits + kWords;
     uint32_t *bcnt = sh + 128, *boff = bcnt + kMaxBuckets;  // (bucketed rows; past the scan words)
+    // the flattened walk's per-wave region (its markers start clear), past the bucket counters
+    constexpr uint32_t kFlat = fr_flat_bytes<S, true, I>();
+    uint8_t *wl = (uint8_t *)(boff + kMaxBuckets) + (threadIdx.x / kWave) * kFlat;
+    if constexpr (!Sem::kOrdered) ((uint32_t *)(wl + kFlat - 4 * kWave))[lane_id()] = 0;
     for (uint32_t w = threadIdx.x; w < CH * Sem::kSlots; w += kFB) acc[w] = V(0);
     for (uint32_t w = threadIdx.x; w < kWords; w += kFB) bits[w] = 0;
     __syncthreads();
@@ -578,7 +706,7 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
                 // skip chunks with no product (mask granule 2^csh columns, a multiple of CH or the last)
                 if (!((cm >> cap63(c0 >> f.csh)) & 1ull)) continue;
                 const uint32_t c1 = (uint32_t)min<uint64_t>(p.ncols, c0 + CH);
-                fr_accumulate<Sem, I>(f, a0, a1, (uint32_t)c0, c1, acc, bits);
+                fr_accumulate<Sem, I>(f, a0, a1, (uint32_t)c0, c1, acc, bits, wl);
                 __syncthreads();
                 emit((uint32_t)c0);
             }
@@ -664,7 +792,8 @@ slat_status slat_fat_symbolic(slat_ctx *ctx, FatArgs &f, const Args &a, bool idx
     static const bool kFull = slat_ab_knob("SLAT_FAT_SYM_FULL") != nullptr;
     const uint64_t sb = kFull ? kSymBits : std::min<uint64_t>(kSymBits, (a.ncols + 2047) / 2048 * 2048);
     f.sym_bits = (uint32_t)sb;
-    const size_t lds = sb / 8 + kFW * 4 + kFW * 8, lds_max = kSymBits / 8 + kFW * 4 + kFW * 8;
+    const size_t flat = (size_t)kFW * fr_flat_bytes<uint32_t, false, uint64_t>();
+    const size_t lds = sb / 8 + kFW * 4 + kFW * 8 + flat, lds_max = kSymBits / 8 + kFW * 4 + kFW * 8 + flat;
     const unsigned per_cu = (unsigned)std::max<size_t>(1, std::min<size_t>(4, (160u * 1024u) / lds));
     const dim3 g((unsigned)ctx->cu_count * per_cu);
     static std::atomic<uint64_t> attr{0};  // devices whose attribute is set (idempotent, so a race is harmless)

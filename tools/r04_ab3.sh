@@ -8,7 +8,7 @@ timeout -k 10 500 python -u -m pytest ${TESTS:-tests/test_spgemm_gpu.py} -m gpu 
 tail -n 2 $OUT/pytest.log
 timeout -k 10 600 python tools/ab.py --reps 2 --steps 100 --chain --sat64 --c4 r3 k5 k5:SLAT_NO_SHORT1=1 > $OUT/ab.txt 2>&1 || { tail -30 $OUT/ab.txt; exit 1; }
 grep -A4 summary $OUT/ab.txt | cut -c1-900
-timeout -k 10 400 python tools/ab_heavy.py --reps 1 r3 k5 > $OUT/heavy.txt 2>&1 || { tail -30 $OUT/heavy.txt; exit 1; }
+timeout -k 10 400 python tools/ab_heavy.py --reps 1 r3 k5 tree > $OUT/heavy.txt 2>&1 || { tail -30 $OUT/heavy.txt; exit 1; }
 tail -n 4 $OUT/heavy.txt | cut -c1-900
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 tools/ab.py --child --steps 20 --chain --c4 > $OUT/child.json 2> $OUT/child.err || { tail -20 $OUT/child.err; exit 1; }
 cat $OUT/child.json
