@@ -736,8 +736,16 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // (MAGNUS's small-row category) when the workgroup kernels take the rest: rows of <= 256 products
     // (a bound: 4 per ELL group) in symbolic, <= 256 outputs in numeric, so every row numeric lists
     // has a stored bitmap. f64 in the fold order keeps one kernel for every row
+    // Only when every row is short by the bound (A's longest row x B's longest row rounded up to ELL
+    // groups <= 256, k_symbolic_short's own bound): with longer rows the window kernels in MODE 2 over
+    // listed rows and the hash path for rows of ~250 outputs measured 2.4x slower on the chain's
+    // A^6 * A (0.153 -> 0.363 ms, profiles/r04_ab3.txt)
     static const bool kNoShort1 = slat_ab_knob("SLAT_NO_SHORT1") != nullptr;
-    const bool short1 = !a.wide && ell && !tiny && !ablate && (dt != SLAT_F64 || f64any) && !kNoShort1;
+    static const bool kShort1Any = slat_ab_knob("SLAT_SHORT1_ANY") != nullptr;  // A/B: the bound not required
+    const bool bound_short = A->max_row_nnz && maxrow_b > 0 &&
+                             (unsigned __int128)A->max_row_nnz * (4 * ((maxrow_b + 3) / 4)) <= kHashT / 2;
+    const bool short1 = !a.wide && ell && !tiny && !ablate && (dt != SLAT_F64 || f64any) && !kNoShort1 &&
+                        (bound_short || kShort1Any);
     const bool hash = (asym.wide || short1) && !kNoHash;
     if (hash) {
         if (asym.wide) a.ww = std::min<uint32_t>(a.ww, 1024);
@@ -769,7 +777,11 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             // tiles of fewer rows when 64-row tiles would leave most resident waves idle (27 000 rows:
             // 422 tiles for ~6 000 waves): about 4 tiles per CU slot of 16 waves
             const uint64_t t = (n + (uint64_t)ctx->cu_count * 16 - 1) / ((uint64_t)ctx->cu_count * 16);
-            a.tile_rows = asym.tile_rows = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, t));
+            static const uint32_t kTileRows = [] {  // A/B knob: rows per tile (8 .. 64)
+                const char *e = slat_ab_knob("SLAT_TILE_ROWS");
+                return e ? (uint32_t)std::min(64, std::max(8, std::atoi(e))) : 0u;
+            }();
+            a.tile_rows = asym.tile_rows = kTileRows ? kTileRows : (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, t));
         }
     }
     // every row short (single-window launches): A's longest row x B's longest row rounded up to ELL
@@ -777,8 +789,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // no row and the window launches are skipped; numeric's short launch stores the completion word
     // (C1: A^2 of the 30^3 torus, 7 x 8 = 56 products a row)
     // (maxrow_b > 0: with an empty B the bound says nothing about a row's entry count)
-    const bool all_short = sym_batched && batched && !asym.wide && A->max_row_nnz && maxrow_b > 0 &&
-                           (unsigned __int128)A->max_row_nnz * (4 * ((maxrow_b + 3) / 4)) <= kHashT / 2;
+    const bool all_short = sym_batched && batched && !asym.wide && bound_short;
     const size_t hash_lds =
         (size_t)wpb * (dt == SLAT_U32    ? (!batched ? hash_bytes<SemU32>() : short_bytes<SemU32>())
                        : dt == SLAT_SAT64 ? (!batched ? hash_bytes<SemSat64>() : short_bytes<SemSat64>())
