@@ -697,7 +697,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                       !(flags & (SLAT_FLAG_TIMING | SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) &&
                       g_progress.load(std::memory_order_relaxed) == 0 &&
                       (unsigned __int128)a_nnz_block * maxrow_b <= (1u << 18) &&
-                      (A->max_row_nnz ? (unsigned __int128)A->max_row_nnz * maxrow_b < slat_fat_min() : maxrow_b <= 32);
+                      (A->max_row_nnz ? (unsigned __int128)A->max_row_nnz * maxrow_b < slat_fat_min(false) : maxrow_b <= 32);
     static const bool kNoEll = slat_ab_knob("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
@@ -736,16 +736,19 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // (MAGNUS's small-row category) when the workgroup kernels take the rest: rows of <= 256 products
     // (a bound: 4 per ELL group) in symbolic, <= 256 outputs in numeric, so every row numeric lists
     // has a stored bitmap. f64 in the fold order keeps one kernel for every row
-    // Only when every row is short by the bound (A's longest row x B's longest row rounded up to ELL
-    // groups <= 256, k_symbolic_short's own bound): with longer rows the window kernels in MODE 2 over
-    // listed rows and the hash path for rows of ~250 outputs measured 2.4x slower on the chain's
-    // A^6 * A (0.153 -> 0.363 ms, profiles/r04_ab3.txt)
-    static const bool kNoShort1 = slat_ab_knob("SLAT_NO_SHORT1") != nullptr;
-    static const bool kShort1Any = slat_ab_knob("SLAT_SHORT1_ANY") != nullptr;  // A/B: the bound not required
+    // Off by default (SLAT_SHORT1=1: on when every row is short by the bound, A's longest row x B's
+    // longest row rounded up to ELL groups <= 256; SLAT_SHORT1_ANY=1: on for any single-window launch).
+    // Measured slower everywhere on the 30^3 chain: with long rows among them, MODE 2 over listed rows
+    // plus the hash path for rows of ~250 outputs took A^6 * A from 0.153 to 0.363 ms
+    // (profiles/r04_ab3.txt); on C1 (A * A, every row short) the 8-row hash batches cost ~56 k cycles
+    // each (a chain of dependent loads, then the 256-key sort) and numeric took 110 us against the
+    // window kernel's 46 (profiles/r04_inv1.txt)
+    static const bool kShort1 = slat_ab_knob("SLAT_SHORT1") != nullptr;
+    static const bool kShort1Any = slat_ab_knob("SLAT_SHORT1_ANY") != nullptr;
     const bool bound_short = A->max_row_nnz && maxrow_b > 0 &&
                              (unsigned __int128)A->max_row_nnz * (4 * ((maxrow_b + 3) / 4)) <= kHashT / 2;
-    const bool short1 = !a.wide && ell && !tiny && !ablate && (dt != SLAT_F64 || f64any) && !kNoShort1 &&
-                        (bound_short || kShort1Any);
+    const bool short1 = !a.wide && ell && !tiny && !ablate && (dt != SLAT_F64 || f64any) &&
+                        ((kShort1 && bound_short) || kShort1Any);
     const bool hash = (asym.wide || short1) && !kNoHash;
     if (hash) {
         if (asym.wide) a.ww = std::min<uint32_t>(a.ww, 1024);
@@ -765,8 +768,13 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // short rows batched several per hash table (integer semirings with the ELL copy of B), else
     // one row per table; composite (row, column) keys need the column bits + 6 <= 31
     // symbolic batches for every value type (it never reads values); numeric for the integer ones
+    // B in CSR form (rows past the ELL limit: power-law graphs) batches the same way, reading its
+    // groups of 4 where they lie (u32 entry offsets: B of < 2^32 entries; SLAT_NO_CSR_BATCH: one
+    // row per table, A/B)
     static const bool kNoBatch = slat_ab_knob("SLAT_NO_BATCH") != nullptr;
-    const bool sym_batched = hash && ell && !kNoBatch;
+    static const bool kNoCsrBatch = slat_ab_knob("SLAT_NO_CSR_BATCH") != nullptr;
+    const bool csr_batch = !ell && !kNoCsrBatch && B->nnz < 0xFFFFFFF0ull;
+    const bool sym_batched = hash && (ell || csr_batch) && !kNoBatch;
     const bool batched = sym_batched && (dt != SLAT_F64 || f64any);
     if (sym_batched) {
         uint32_t cb = 1;
@@ -839,7 +847,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // max row of A x max row of B (A's max row unknown: when B has long rows)
     static const bool kNoFat = slat_ab_knob("SLAT_NO_FAT") != nullptr;
     const uint64_t maxrow_a = A->max_row_nnz;
-    const bool fat = !kNoFat && !tiny && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= slat_fat_min() : maxrow_b > 32);
+    const uint64_t fat_min = slat_fat_min(!ell && (dt != SLAT_F64 || f64any));
+    const bool fat = !kNoFat && !tiny && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= fat_min : maxrow_b > 32);
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
@@ -1000,7 +1009,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     slat::FatArgs fat_args = {};
     slat::FatArgs *fa = &fat_args;
     if (fat) {
-        if ((st = slat_fat_select(ctx, a, ws + o_fat, fa))) return failc(st);
+        if ((st = slat_fat_select(ctx, a, ws + o_fat, fat_min, fa))) return failc(st);
         fa->buckets = (flags & SLAT_FLAG_FAT_BUCKETS) ? 1u : 0u;
         asym.fr_mark = a.fr_mark;
     }
@@ -1038,7 +1047,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         h1.list_cnt = h2.list_cnt = lc;
         const uint64_t trows = h1.tile_rows ? h1.tile_rows : kWave;
         const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + trows - 1) / trows / wpb + 1, ctx->cu_count * 16ull)));
-        SLAT_HIPC(slat_launch_symbolic_short(idx32, g1, wpb * sym_short_bytes(), s, h1));
+        SLAT_HIPC(slat_launch_symbolic_short(idx32, ell, g1, wpb * sym_short_bytes(), s, h1));
         h2.tq = (kDyn & 2u) && asym.wide ? tq : nullptr;  // (single-window rows: a fixed stride)
         if (all_short) {
             // (no listed rows)

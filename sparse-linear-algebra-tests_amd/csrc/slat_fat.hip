@@ -727,15 +727,19 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
 
 using namespace slat;
 
-// products per row from which a row is fat: 8192 (16384 until round 3: rows between went to the window
-// pass's global-atomic hub path; 8192 measured R-MAT 2^16 A^2 numeric 8.67 -> 8.17 ms, C5 2^16 fold
-// 15.8 -> 13.7 ms, 2^18 fold 121 -> 114 ms, profiles/r03_ab_fat_min.txt; SLAT_FAT_MIN: A/B knob)
-uint64_t slat_fat_min() {
+// products per row from which a row is fat. B in CSR form (rows past the ELL limit: power-law
+// graphs) and a semiring that adds with atomics: 2048 since the flattened walk (round 4: R-MAT 2^16
+// A^2 7.56 -> 6.65 ms, C5 2^16 any order 8.51 -> 6.98, 2^18 any 45.7 -> 45.1 against 8192; 1024 and
+// 512 measured between, profiles/r04_inv1.txt). Otherwise 8192 (16384 until round 3,
+// r03_ab_fat_min.txt): f64 in the reference's fold order keeps the ordered per-slice walk, and ELL
+// launches (short B rows, the 30^3 chain) keep their rows in the window kernels.
+// SLAT_FAT_MIN: A/B knob (both cases)
+uint64_t slat_fat_min(bool flat) {
     static const uint64_t v = [] {
         const char *e = slat_ab_knob("SLAT_FAT_MIN");
-        return e ? std::max<uint64_t>(256, std::strtoull(e, nullptr, 10)) : 8192ull;
+        return e ? std::max<uint64_t>(256, std::strtoull(e, nullptr, 10)) : 0ull;
     }();
-    return v;
+    return v ? v : flat ? 2048ull : 8192ull;
 }
 
 // workspace bytes of the fat-row category for n rows
@@ -751,7 +755,7 @@ size_t slat_fat_ws(uint64_t n) { return ((n + 255) & ~255ull) * (1 + 4 + 8) + 25
 
 // Select the fat rows (marks into a.fr_mark's buffer) and count them on the device; nothing to do on
 // the host. `ws` = slat_fat_ws(n) bytes of workspace.
-slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
+slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, uint64_t fat_min, FatArgs *out) {
     const hipStream_t s = ctx->stream;
     const uint64_t n = a.nrows;
     const uint64_t nn = (n + 255) & ~255ull;
@@ -773,7 +777,7 @@ slat_status slat_fat_select(slat_ctx *ctx, Args &a, void *ws, FatArgs *out) {
     f.bval = nullptr;
     f.bcap = 0;
     f.tq = ctx->d_words + 5;
-    f.fat_min = slat_fat_min();
+    f.fat_min = fat_min;
     f.buckets = 0;
     SLAT_HIP(ctx, hipMemsetAsync(f.cnt, 0, 4, s));
     a.fr_mark = f.mark;

@@ -28,7 +28,7 @@ struct FatArgs {
     // row tickets (SLAT_FAT_TICKET; the context's ticket word, zero between launches): rows by a
     // counter instead of a fixed stride over the blocks
     unsigned long long *tq;
-    uint64_t fat_min;  // products per row from which a row is fat (slat_fat_min())
+    uint64_t fat_min;  // products per row from which a row is fat (slat_fat_min)
     uint32_t sym_bits;  // k_fr_symbolic's bitmap columns per pass (slat_fat_symbolic)
     uint32_t buckets;   // SLAT_FLAG_FAT_BUCKETS: products bucketed by chunk in HBM (fr_num)
 };
@@ -38,11 +38,12 @@ struct FatArgs {
 // in B row k of its first column >= g << shift, g in [0, nch1) (the last = the row's length)
 hipError_t slat_launch_splits(slat_ctx *ctx, const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb, uint32_t nch1,
                               uint32_t shift, uint32_t *split, hipStream_t s);
-// products per row from which a row takes the fat-row kernels (8192)
-uint64_t slat_fat_min();
+// products per row from which a row takes the fat-row kernels: 2048 with `flat` (B in CSR form, a
+// semiring that adds with atomics: the flattened walk), else 8192
+uint64_t slat_fat_min(bool flat);
 // workspace bytes of the category for n rows
 size_t slat_fat_ws(uint64_t n);
-// mark and list the rows of >= slat_fat_min() products (sets a.fr_mark); nothing comes back to the host
-slat_status slat_fat_select(slat_ctx *ctx, slat::Args &a, void *ws, slat::FatArgs *out);
+// mark and list the rows of >= fat_min products (sets a.fr_mark); nothing comes back to the host
+slat_status slat_fat_select(slat_ctx *ctx, slat::Args &a, void *ws, uint64_t fat_min, slat::FatArgs *out);
 slat_status slat_fat_symbolic(slat_ctx *ctx, slat::FatArgs &f, const slat::Args &a, bool idx32);
 slat_status slat_fat_numeric(slat_ctx *ctx, slat::FatArgs &f, const slat::Args &a, int32_t dtype, bool f64any, bool idx32);

@@ -57,7 +57,8 @@ hipError_t slat_launch_symbolic(int mode, bool idx32, bool ell, dim3 grid, size_
 hipError_t slat_launch_tiny(int sem, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a,
                             unsigned long long *status, uint32_t epoch, unsigned long long *maxw);
 // the batched short-row symbolic of wide launches (lists the other rows for mode 2)
-hipError_t slat_launch_symbolic_short(bool idx32, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
+// (ell: B's ELL image; else B read in CSR form, < 2^32 entries)
+hipError_t slat_launch_symbolic_short(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
 
 // a workgroup per row (slat_group.hip): single-window launches with B in ELL form. Symbolic for every
 // value type (it reads no values); numeric for u32, Sat64 and f64 in any order (sem ids above)

@@ -21,11 +21,13 @@ using Sem = std::conditional_t<SLAT_SEM == kSemU32, SemU32,
 // the instance of (mode, offsets, B form); F(kernel) is called with its function pointer
 template <typename F>
 hipError_t with_instance(int mode, bool idx32, bool ell, F &&f) {
-    if (mode == 3) {  // batched short rows (integer semirings and f64 in any order, ELL B)
+    if (mode == 3) {  // batched short rows (integer semirings and f64 in any order; B as ELL or CSR)
         if constexpr (std::is_same_v<Sem, SemU32>)
-            return idx32 ? f(k_numeric_short_u32<uint32_t>) : f(k_numeric_short_u32<uint64_t>);
+            return idx32 ? (ell ? f(k_numeric_short_u32<uint32_t, false>) : f(k_numeric_short_u32<uint32_t, true>))
+                         : (ell ? f(k_numeric_short_u32<uint64_t, false>) : f(k_numeric_short_u32<uint64_t, true>));
         else if constexpr (!Sem::kOrdered)
-            return idx32 ? f(k_numeric_short<Sem, uint32_t>) : f(k_numeric_short<Sem, uint64_t>);
+            return idx32 ? (ell ? f(k_numeric_short<Sem, uint32_t, false>) : f(k_numeric_short<Sem, uint32_t, true>))
+                         : (ell ? f(k_numeric_short<Sem, uint64_t, false>) : f(k_numeric_short<Sem, uint64_t, true>));
         else
             return hipErrorInvalidValue;
     }

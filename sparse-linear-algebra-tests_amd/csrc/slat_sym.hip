@@ -22,10 +22,17 @@ hipError_t slat_launch_symbolic(int mode, bool idx32, bool ell, dim3 grid, size_
                  : (ell ? go(k_symbolic<uint64_t, true>) : go(k_symbolic<uint64_t, false>));
 }
 
-hipError_t slat_launch_symbolic_short(bool idx32, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
-    if (idx32)
-        hipLaunchKernelGGL(k_symbolic_short<uint32_t>, grid, dim3(kBlock), lds, s, a);
-    else
-        hipLaunchKernelGGL(k_symbolic_short<uint64_t>, grid, dim3(kBlock), lds, s, a);
+hipError_t slat_launch_symbolic_short(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const Args &a) {
+    if (idx32) {
+        if (ell)
+            hipLaunchKernelGGL((k_symbolic_short<uint32_t, false>), grid, dim3(kBlock), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_symbolic_short<uint32_t, true>), grid, dim3(kBlock), lds, s, a);
+    } else {
+        if (ell)
+            hipLaunchKernelGGL((k_symbolic_short<uint64_t, false>), grid, dim3(kBlock), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_symbolic_short<uint64_t, true>), grid, dim3(kBlock), lds, s, a);
+    }
     return hipGetLastError();
 }

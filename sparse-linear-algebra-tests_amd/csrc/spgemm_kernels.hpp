@@ -575,6 +575,47 @@ __device__ __forceinline__ uint4 ell_cols(const Args &p, uint32_t k, uint32_t t)
     return *(const uint4 *)((const uint8_t *)p.ell_col + off);
 }
 
+// The short-row kernels over B in CSR form (wide launches whose B rows outgrow the ELL image: power-law
+// graphs): a "group" is up to 4 consecutive entries of a B row, staged as the offset of its first entry
+// in B (u32: the host takes this form only for B of < 2^32 entries) and its entry count - 1 in bits
+// 6-7 of the local-row byte. The entries are read where they lie, no image is built.
+__device__ __forceinline__ uint4 csr_cols(const Args &p, uint32_t off, uint32_t cnt) {
+    const uint32_t *c = p.b_col + off;
+    uint4 r;
+    r.x = c[0];
+    r.y = cnt > 1 ? c[1] : kSent;
+    r.z = cnt > 2 ? c[2] : kSent;
+    r.w = cnt > 3 ? c[3] : kSent;
+    return r;
+}
+template <typename S>
+__device__ __forceinline__ Quad<S> csr_vals(const Args &p, uint32_t off, uint32_t cnt) {
+    const S *v = (const S *)p.b_val + off;
+    Quad<S> q;
+    q.v[0] = v[0];
+    q.v[1] = cnt > 1 ? v[1] : S(0);
+    q.v[2] = cnt > 2 ? v[2] : S(0);
+    q.v[3] = cnt > 3 ? v[3] : S(0);
+    return q;
+}
+// an A entry's B row for the short-row kernels: ELL, its group count; CSR, k becomes the row's first
+// entry offset and the count its length (groups = (len + 3) / 4). kSent / out of range: count 0
+template <bool CSR>
+__device__ __forceinline__ uint32_t short_brow(const Args &p, uint32_t &k) {
+    if (k >= p.b_nrows) return 0u;
+    if constexpr (CSR) {
+        const uint64_t r0 = p.b_rp[k], r1 = p.b_rp[k + 1];
+        k = (uint32_t)r0;
+        return (uint32_t)min<uint64_t>(r1 - r0, 1u << 30);
+    } else {
+        return p.ell_ng[k];
+    }
+}
+template <bool CSR>
+__device__ __forceinline__ uint32_t short_groups(uint32_t cnt) {
+    return CSR ? (cnt + 3) >> 2 : cnt;
+}
+
 // ------------------------------------------------------------------------------------------------
 // group walks: the passes consume B entries four at a time (one ELL group, or a CSR entry padded
 // with kSent), branch-free inside a group, so a wave issues every LDS access of a group before
@@ -2012,21 +2053,42 @@ __device__ __forceinline__ uint32_t group_positions(const uint32_t (&ng)[kRegQ],
 // a quarter of the lanes): gk = B row | group << 24 (B rows < 2^24 with the ELL copy), gl = local
 // row, ga = A value.
 constexpr uint32_t kStageG = 256;
-template <bool VALS, typename S>
+// (CSR: kq = the B row's first entry offset, cnt = its length; ELL: kq = the B row, cnt = its groups)
+template <bool VALS, bool CSR, typename S>
 __device__ __forceinline__ void stage_groups(uint32_t base, uint32_t mxg, const uint32_t (&kq)[kRegQ],
-                                             const uint32_t (&lq)[kRegQ], const uint32_t (&ng)[kRegQ],
+                                             const uint32_t (&lq)[kRegQ], const uint32_t (&cnt)[kRegQ],
                                              const uint32_t (&pos)[kRegQ], const S (&aq)[kRegQ], uint32_t *gk,
                                              uint8_t *gl, S *ga) {
     for (uint32_t t = 0; t < mxg; ++t)
         sfor<kRegQ>([&](auto Q) {
             const uint32_t g = pos[Q] + t - base;  // wraps past kStageG below base
-            if (t < ng[Q] && g < kStageG) {
-                gk[g] = kq[Q] | (t << 24);
-                gl[g] = (uint8_t)lq[Q];
+            if (t < short_groups<CSR>(cnt[Q]) && g < kStageG) {
+                if constexpr (CSR) {
+                    gk[g] = kq[Q] + 4 * t;
+                    gl[g] = (uint8_t)(lq[Q] | ((min(4u, cnt[Q] - 4 * t) - 1) << 6));
+                } else {
+                    gk[g] = kq[Q] | (t << 24);
+                    gl[g] = (uint8_t)lq[Q];
+                }
                 if constexpr (VALS) ga[g] = aq[Q];
             }
         });
     wave_sync();
+}
+// a staged group's columns (kSent past its entries) and its local row
+template <bool CSR>
+__device__ __forceinline__ uint4 staged_cols(const Args &p, uint32_t w, uint32_t glb) {
+    if constexpr (CSR)
+        return csr_cols(p, w, (glb >> 6) + 1);
+    else
+        return ell_cols(p, w & 0xFFFFFFu, w >> 24);
+}
+template <bool CSR, typename S>
+__device__ __forceinline__ Quad<S> staged_vals(const Args &p, uint32_t w, uint32_t glb) {
+    if constexpr (CSR)
+        return csr_vals<S>(p, w, (glb >> 6) + 1);
+    else
+        return ell_vals<S>(p, w & 0xFFFFFFu, w >> 24);
 }
 
 // MAGNUS row categorisation input: the ELL groups of each row of a 64-row tile (lane j: row r0 + j),
@@ -2035,6 +2097,7 @@ __device__ __forceinline__ void stage_groups(uint32_t base, uint32_t mxg, const 
 // of <= 256 entries use the difference, and the entries of longer rows are skipped, not read).
 // pf: u32[256] of LDS, left dirty.
 // Rows of more than `jump` entries are jumped over (their bound is never needed: they are long).
+template <bool CSR>
 __device__ __forceinline__ uint32_t tile_groups(const Args &p, uint64_t A0j, uint64_t A1j, uint32_t nt, uint32_t *pf,
                                                 uint64_t jump = 256) {
     const uint32_t lane = (uint32_t)lane_id();
@@ -2054,7 +2117,7 @@ __device__ __forceinline__ uint32_t tile_groups(const Args &p, uint64_t A0j, uin
             const uint64_t idx = c0 + Q * kWave + lane;
             kk[Q] = idx < T1 ? p.a_col[idx] : kSent;
         });
-        sfor<4>([&](auto Q) { g[Q] = kk[Q] < p.b_nrows ? (uint32_t)p.ell_ng[kk[Q]] : 0u; });
+        sfor<4>([&](auto Q) { g[Q] = short_groups<CSR>(short_brow<CSR>(p, kk[Q])); });
         sfor<4>([&](auto Q) {
             const uint32_t incl = wave_incl_scan(g[Q], 0u, [](uint32_t x, uint32_t y) { return x + y; });
             pf[Q * kWave + lane] = run + incl - g[Q];
@@ -2078,7 +2141,7 @@ __device__ __forceinline__ uint32_t tile_groups(const Args &p, uint64_t A0j, uin
 // gk u32[kStageG], gl u8[kStageG]
 __host__ __device__ constexpr uint32_t sym_short_bytes() { return kSymHashT * 4 + 256 * 4 + kWave * 4 + kStageG * 5; }
 
-template <typename I>
+template <typename I, bool CSR = false>
 __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
     constexpr int kWpb = kBlock / kWave;
     const uint32_t kCap = p.sym_cap ? p.sym_cap : kSymHashT * SLAT_SYM_CAP_PCT / 100;
@@ -2118,7 +2181,7 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
         // long without reading its entries (bound >= 4 per entry with a non-empty B row; a row sent
         // long with empty B rows among its entries is still correct, only another category)
         const uint64_t jump = p.sym_cap ? (uint64_t)kCap / 4 : 256;
-        const uint32_t gj = tile_groups(p, A0j, A1j, nt, marks, jump);
+        const uint32_t gj = tile_groups<CSR>(p, A0j, A1j, nt, marks, jump);
         const uint32_t bj = gj > 0x3FFFFFFFu ? 0xFFFFFFFFu : 4 * gj;
         ((uint4 *)marks)[lane] = make_uint4(0, 0, 0, 0);
         wave_sync();
@@ -2161,25 +2224,27 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
                     marks[i] = 0;
                 }
             });
+            // (ng: ELL, the B row's groups; CSR, its length, and kq its first entry)
+            uint32_t gq[kRegQ];
             sfor<kRegQ>([&](auto Q) {
-                if (kq[Q] >= p.b_nrows) kq[Q] = kSent;
-                ng[Q] = kq[Q] != kSent ? p.ell_ng[kq[Q]] : 0u;
-                mxg = max(mxg, ng[Q]);
+                ng[Q] = short_brow<CSR>(p, kq[Q]);
+                gq[Q] = short_groups<CSR>(ng[Q]);
+                mxg = max(mxg, gq[Q]);
             });
             mxg = wave_max_u32(mxg);
             uint32_t nprod = 0, pos[kRegQ];
-            const uint32_t G = group_positions(ng, pos);
+            const uint32_t G = group_positions(gq, pos);
             const uint32_t noval[kRegQ] = {};
             for (uint32_t base = 0; base < G; base += kStageG) {
-                stage_groups<false, uint32_t>(base, mxg, kq, lq, ng, pos, noval, gk, gl, nullptr);
+                stage_groups<false, CSR, uint32_t>(base, mxg, kq, lq, ng, pos, noval, gk, gl, nullptr);
                 const uint32_t n = min(G - base, kStageG);
                 for (uint32_t g0 = 0; g0 < n; g0 += kWave) {
                     const uint32_t g = g0 + lane;
                     uint32_t cc[4] = {kSent, kSent, kSent, kSent}, sl[4], lr = 0;
                     if (g < n) {
-                        const uint32_t w = gk[g];
-                        const uint4 c = ell_cols(p, w & 0xFFFFFFu, w >> 24);
-                        lr = gl[g];
+                        const uint32_t w = gk[g], glb = gl[g];
+                        const uint4 c = staged_cols<CSR>(p, w, glb);
+                        lr = glb & 63u;
                         const uint32_t hi = lr << cb;
                         cc[0] = c.x != kSent ? (hi | c.x) : kSent;
                         cc[1] = c.y != kSent ? (hi | c.y) : kSent;
@@ -2379,7 +2444,7 @@ __device__ __forceinline__ void batch_emit(uint32_t *hkeys, typename Sem::V *hva
     wave_sync();
 }
 
-template <typename Sem0, typename I>
+template <typename Sem0, typename I, bool CSR>
 __device__ __forceinline__ void numeric_short_body(Args p) {
     using Sem = ShortSem<Sem0>;
     using S = typename Sem::S;
@@ -2500,15 +2565,21 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
                     marks[i] = 0;
                 }
             });
+            // (ng: ELL, the B row's groups; CSR, its length, and kq its first entry; malformed
+            // entries: 0)
             sfor<kRegQ>([&](auto Q) {
-                if (kq[Q] >= p.b_nrows) kq[Q] = kSent;  // malformed input: ignore the entry
-                ng[Q] = kq[Q] != kSent ? p.ell_ng[kq[Q]] : 0u;
-                mxg = max(mxg, ng[Q]);
+                ng[Q] = short_brow<CSR>(p, kq[Q]);
+                mxg = max(mxg, short_groups<CSR>(ng[Q]));
             });
             mxg = wave_max_u32(mxg);
             pc.mark(1);  // A entries, local rows, group counts
             uint32_t pos[kRegQ];
-            const uint32_t G = group_positions(ng, pos);
+            uint32_t G;
+            {
+                uint32_t gq[kRegQ];
+                sfor<kRegQ>([&](auto Q) { gq[Q] = short_groups<CSR>(ng[Q]); });
+                G = group_positions(gq, pos);
+            }
             bool narrow = false;  // u32: no sum of this batch can wrap (each key takes <= G products)
             if constexpr (std::is_same_v<Sem, SemU32W>) {
                 if (bvmax) {
@@ -2519,18 +2590,18 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
                 }
             }
             for (uint32_t base = 0; base < G; base += kStageG) {
-                stage_groups<true, S>(base, mxg, kq, lq, ng, pos, aq, gk, gl, ga);
+                stage_groups<true, CSR, S>(base, mxg, kq, lq, ng, pos, aq, gk, gl, ga);
                 const uint32_t n = min(G - base, kStageG);
                 for (uint32_t g0 = 0; g0 < n; g0 += kWave) {
                     const uint32_t g = g0 + lane;
                     uint4 ck = make_uint4(kSent, kSent, kSent, kSent);
                     Quad<S> pr{};
                     if (g < n) {
-                        const uint32_t w = gk[g], bk = w & 0xFFFFFFu, t = w >> 24;
-                        const uint4 c = ell_cols(p, bk, t);
+                        const uint32_t w = gk[g], glb = gl[g];
+                        const uint4 c = staged_cols<CSR>(p, w, glb);
                         const S a = ga[g];
-                        pr = buni ? splat4(Sem::prod(a, bv0)) : prods<Sem>(a, ell_vals<S>(p, bk, t));
-                        const uint32_t hi = (uint32_t)gl[g] << cb;
+                        pr = buni ? splat4(Sem::prod(a, bv0)) : prods<Sem>(a, staged_vals<CSR, S>(p, w, glb));
+                        const uint32_t hi = (glb & 63u) << cb;
                         ck.x = c.x != kSent ? (hi | c.x) : kSent;
                         ck.y = c.y != kSent ? (hi | c.y) : kSent;
                         ck.z = c.z != kSent ? (hi | c.z) : kSent;
@@ -2578,9 +2649,9 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
     add_zero_rows(&p.host_out[2], wave_sum_u32(zrows), p.seq != 0);
 }
 
-template <typename Sem0, typename I>
+template <typename Sem0, typename I, bool CSR = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_numeric_short(Args p) {
-    numeric_short_body<Sem0, I>(p);
+    numeric_short_body<Sem0, I, CSR>(p);
     signal_done(p);
 }
 // u32: 5 waves per SIMD (6.6 KB of LDS per wave, <= 96 VGPRs; the wider semirings are held to 4
@@ -2590,13 +2661,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 #ifndef SLAT_SHORT_WPE
 #define SLAT_SHORT_WPE 5
 #endif
-template <typename I>
+template <typename I, bool CSR = false>
 __global__ __launch_bounds__(kBlock)
 #if SLAT_SHORT_WPE
 __attribute__((amdgpu_waves_per_eu(SLAT_SHORT_WPE)))
 #endif
 void k_numeric_short_u32(Args p) {
-    numeric_short_body<SemU32, I>(p);
+    numeric_short_body<SemU32, I, CSR>(p);
     signal_done(p);
 }
 

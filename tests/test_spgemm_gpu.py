@@ -443,3 +443,44 @@ def test_single_window_short_row_categories(ctx, case, dtype):
         b = O.from_coo(n, br, bc, bv, DT[dtype])
     got = to_dev(a, dtype)._spgemm(to_dev(b, dtype))
     assert_same(got, O.matmul_seq(a, b), f"single-window {case}")
+
+
+@pytest.mark.parametrize("dtype", [slat.U32, slat.SAT64, slat.F64])
+@pytest.mark.parametrize("vals", ["small", "big", "zeros"])
+def test_wide_csr_b_short_row_batches(ctx, dtype, vals):
+    """Wide launches (columns past one LDS window) whose B has rows longer than the ELL image allows
+    read B in CSR form; their short rows are batched in the hash tables all the same, each B row's
+    entries taken 4 at a time where they lie (the last group partial: rows of 1..9 entries and a few
+    of 40..300, so groups of every count 1..4). big: products and sums past 2^32 (u32 saturates);
+    zeros: explicit zero B values (the zero-row count)."""
+    rng = np.random.default_rng({"small": 11, "big": 12, "zeros": 13}[vals])
+    n = 70_000
+    lens = rng.integers(0, 6, n)
+    lens[::1000] = 40  # a few medium A rows (window category)
+    ar = np.repeat(np.arange(n), lens)
+    ac = np.concatenate([rng.choice(n, k, replace=False) for k in lens])
+    bl = rng.integers(1, 10, n)
+    bl[::997] = rng.integers(40, 300, len(bl[::997]))  # B rows past the ELL limit (32)
+    br = np.repeat(np.arange(n), bl)
+    bc = np.concatenate([rng.choice(n, k, replace=False) for k in bl])
+    hi = {"small": 7, "big": (1 << 31) + 7, "zeros": 3}[vals]
+    lo = 0 if vals == "zeros" else 1
+    if dtype == slat.F64:
+        av, bv = rng.standard_normal(len(ar)), rng.standard_normal(len(br))
+        if vals == "zeros":
+            bv[::5] = 0.0
+    else:
+        av, bv = rng.integers(1, hi, len(ar)), rng.integers(lo, hi, len(br))
+    a = O.from_coo(n, ar, ac, av, DT[dtype])
+    b = O.from_coo(n, br, bc, bv, DT[dtype])
+    flags = slat.FLAG_F64_ANY_ORDER if dtype == slat.F64 else 0
+    got = to_dev(a, dtype)._spgemm(to_dev(b, dtype), flags)
+    want = O.matmul_seq(a, b)
+    if dtype == slat.F64:  # any order: within rtol 1e-12 of the fold order
+        h = got.host()
+        rp, col, val = want.arrays()
+        np.testing.assert_array_equal(h.row_ptr, rp)
+        np.testing.assert_array_equal(h.col_idx, col)
+        np.testing.assert_allclose(h.values, val, rtol=1e-12, atol=1e-12)
+    else:
+        assert_same(got, want, f"wide CSR-B short batches {vals}")
