@@ -66,7 +66,7 @@ __host__ __device__ constexpr uint32_t fr_flat_bytes() {
 template <typename Sem>
 __host__ __device__ constexpr size_t fr_lds() {
     return (size_t)fr_chunk<Sem>() * sizeof(typename Sem::V) * Sem::kSlots + fr_chunk<Sem>() / 8 + 64 * 8 +
-           (Sem::kOrdered ? 0 : 2 * kMaxBuckets * 4 + kFW * fr_flat_bytes<typename Sem::S, true, uint64_t>());
+           (Sem::kOrdered ? 0 : 2 * kMaxBuckets * 4) + kFW * fr_flat_bytes<typename Sem::S, true, uint64_t>();
 }
 
 __device__ __forceinline__ uint32_t cap63(uint64_t x) { return x < 63 ? (uint32_t)x : 63u; }
@@ -267,7 +267,11 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
 #define SLAT_FR_FLAT 1
 #endif
 constexpr uint32_t kFlatHuge = 1u << 24;  // parts at least this long: walked by the whole wave alone
-template <typename S, bool VALS, typename I, typename Part, typename F>
+// ORDERED (f64 in the reference's fold order): the wave walks every entry of the row itself, in A
+// order (each wave owns its own slice of the chunk's columns), and fn(c, a, b, valid) is called by the
+// whole wave once per slot of 64 products, slots in position order, so it can keep each column's
+// products in entry order; otherwise fn(c, a, b) per product.
+template <typename S, bool VALS, typename I, bool ORDERED = false, typename Part, typename F>
 __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, F &&fn, uint8_t *wl) {
     const int lane = lane_id();
     const int wv = threadIdx.x / kWave;
@@ -278,9 +282,11 @@ __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, 
     const S *bv = (const S *)p.b_val;
     const auto plus = [](uint32_t x, uint32_t y) { return x + y; };
     const auto mx = [](uint32_t x, uint32_t y) { return max(x, y); };
-    // wave w's entries: w, w + 8, w + 16, ... (a row of 100 entries keeps all 8 waves busy)
-    for (I base = a0 + (I)wv; base < a1; base += (I)kFB) {
-        const I i = base + (I)lane * (I)kFW;
+    // wave w's entries: w, w + 8, w + 16, ... (a row of 100 entries keeps all 8 waves busy);
+    // ORDERED: all of them, 64 at a time
+    constexpr I kStep = ORDERED ? (I)kWave : (I)kFB;
+    for (I base = a0 + (ORDERED ? (I)0 : (I)wv); base < a1; base += kStep) {
+        const I i = base + (I)lane * (ORDERED ? (I)1 : (I)kFW);
         I bs = 0;
         uint32_t len = 0;
         S a = S(0);
@@ -289,7 +295,9 @@ __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, 
             if constexpr (VALS) a = av[i];
             if (k < p.b_nrows) part(k, bs, len);
         }
-        // a part of 2^24 or more entries on its own (the flat offsets stay below 2^30)
+        // a part of 2^24 or more entries on its own (the flat offsets stay below 2^30; an ordered
+        // slice part is at most the slice's width)
+        if constexpr (!ORDERED)
         for (unsigned long long m = __ballot(len >= kFlatHuge); m; m &= m - 1) {
             const int l0 = (int)__builtin_ctzll(m);
             const I s0 = (I)readlane_u64((uint64_t)bs, l0);
@@ -330,9 +338,12 @@ __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, 
                     }
                 }
             });
-            sfor<4>([&](auto E) {
-                if (c[E] != kSent) fn(c[E], aa[E], v[E]);
-            });
+            if constexpr (ORDERED)
+                sfor<4>([&](auto E) { fn(c[E], aa[E], v[E], c[E] != kSent); });
+            else
+                sfor<4>([&](auto E) {
+                    if (c[E] != kSent) fn(c[E], aa[E], v[E]);
+                });
             wave_sync();  // the markers clear before the next pass writes them
         }
     }
@@ -496,6 +507,43 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
         const int lane = lane_id(), wv = threadIdx.x / kWave;
         const uint32_t g = g0 + (uint32_t)wv;
         if ((c0 + ((uint32_t)wv << f.gsh)) >= c1) return;
+        if constexpr (SLAT_FR_FLAT) {
+            // the wave's slice flattened over the row's entries (every lane on a product, whatever
+            // the parts' lengths), slots of 64 products in A order. Within a slot the lanes are in
+            // position order, so lanes on one column apply their products lowest lane first: the
+            // column's same-column lanes by one ballot per offset bit, then rounds by rank (one round
+            // unless two entries of the slot meet on a column)
+            const uint32_t sw = 1u << f.gsh, s0 = c0 + ((uint32_t)wv << f.gsh);
+            const uint64_t lt = (1ull << lane) - 1;
+            fr_flat<S, true, I, true>(
+                p, a0, a1,
+                [&](uint32_t k, I &bs, uint32_t &len) {
+                    const uint32_t *sp = f.split + (uint64_t)k * f.nch1 + g;
+                    const uint32_t q0 = sp[0];
+                    bs = (I)p.b_rp[k] + (I)q0;
+                    len = sp[1] - q0;
+                },
+                [&](uint32_t c, S a, S b, bool valid) {
+                    const uint32_t ol = valid ? c - s0 : 0u;  // offset in the slice
+                    unsigned long long same = __ballot(valid);
+                    for (uint32_t bit = 1; bit < sw; bit <<= 1) {
+                        const unsigned long long bb = __ballot(valid && (ol & bit));
+                        same &= (ol & bit) ? bb : ~bb;
+                    }
+                    const uint32_t rank = valid ? (uint32_t)__popcll(same & lt) : 0u;
+                    const uint32_t rmax = wave_max_u32(rank);
+                    const uint32_t o = ol + (s0 - c0);
+                    for (uint32_t r = 0; r <= rmax; ++r) {
+                        if (valid && rank == r) {
+                            acc[o] = __dadd_rn(acc[o], __dmul_rn(a, b));
+                            atomicOr(&bits[o >> 5], 1u << (o & 31));
+                        }
+                        wave_sync();
+                    }
+                },
+                wl);
+            return;
+        }
         for (I base = a0; base < a1; base += (I)kWave) {
             const I i = base + (I)lane;
             S a = S(0);
@@ -654,8 +702,8 @@ __global__ __launch_bounds__(kFB) void k_fr_numeric(FatArgs f) {
     uint32_t *bcnt = sh + 128, *boff = bcnt + kMaxBuckets;  // (bucketed rows; past the scan words)
     // the flattened walk's per-wave region (its markers start clear), past the bucket counters
     constexpr uint32_t kFlat = fr_flat_bytes<S, true, I>();
-    uint8_t *wl = (uint8_t *)(boff + kMaxBuckets) + (threadIdx.x / kWave) * kFlat;
-    if constexpr (!Sem::kOrdered) ((uint32_t *)(wl + kFlat - 4 * kWave))[lane_id()] = 0;
+    uint8_t *wl = (uint8_t *)(Sem::kOrdered ? bcnt : boff + kMaxBuckets) + (threadIdx.x / kWave) * kFlat;  // (fr_lds)
+    ((uint32_t *)(wl + kFlat - 4 * kWave))[lane_id()] = 0;
     for (uint32_t w = threadIdx.x; w < CH * Sem::kSlots; w += kFB) acc[w] = V(0);
     for (uint32_t w = threadIdx.x; w < kWords; w += kFB) bits[w] = 0;
     __syncthreads();
