@@ -271,8 +271,10 @@ constexpr uint32_t kFlatHuge = 1u << 24;  // parts at least this long: walked by
 // order (each wave owns its own slice of the chunk's columns), and fn(c, a, b, valid) is called by the
 // whole wave once per slot of 64 products, slots in position order, so it can keep each column's
 // products in entry order; otherwise fn(c, a, b) per product.
+// uni: every B value equals v0 (a pattern B, from k_bvmax's summary): no B-value loads
 template <typename S, bool VALS, typename I, bool ORDERED = false, typename Part, typename F>
-__device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, F &&fn, uint8_t *wl) {
+__device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, F &&fn, uint8_t *wl, bool uni = false,
+                                        S v0 = S(0)) {
     const int lane = lane_id();
     const int wv = threadIdx.x / kWave;
     I *eb = (I *)wl;
@@ -333,7 +335,7 @@ __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, 
                     const I bi = eb[l] + (I)j;
                     c[E] = p.b_col[bi];
                     if constexpr (VALS) {
-                        v[E] = bv[bi];
+                        v[E] = uni ? v0 : bv[bi];
                         aa[E] = ea[l];
                     }
                 }
@@ -476,6 +478,17 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
     const uint32_t g0 = c0 >> f.gsh, g1 = min(f.nch1 - 1, (c1 + (1u << f.gsh) - 1) >> f.gsh);
     if constexpr (!Sem::kOrdered && SLAT_FR_FLAT) {
         if (f.split) {  // the chunk's part of each B row from the split table: no filtering
+            // a pattern B (every value equal, k_bvmax's epoch-tagged max and ~min): no value loads
+            bool uni = false;
+            S v0 = S(0);
+            if constexpr (Sem::kNarrowable)
+                if (p.b_vmax) {
+                    const unsigned long long vx = ((volatile unsigned long long *)p.b_vmax)[kVMaxWord];
+                    const unsigned long long vi = ((volatile unsigned long long *)p.b_vmax)[kVMinInvWord];
+                    uni = (uint32_t)(vx >> 32) == p.epoch && (uint32_t)(vi >> 32) == p.epoch &&
+                          ~(uint32_t)vi == (uint32_t)vx && (sizeof(S) == 4 || (uint32_t)vx != 0xFFFFFFFFu);
+                    v0 = (S)(uint32_t)vx;
+                }
             fr_flat<S, true, I>(
                 p, a0, a1,
                 [&](uint32_t k, I &bs, uint32_t &len) {
@@ -489,7 +502,7 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                     Sem::acc(acc, o, Sem::prod(a, b));
                     atomicOr(&bits[o >> 5], 1u << (o & 31));
                 },
-                wl);
+                wl, uni, v0);
             return;
         }
     }
