@@ -266,6 +266,9 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
 #ifndef SLAT_FR_FLAT
 #define SLAT_FR_FLAT 1
 #endif
+#ifndef SLAT_FR_FLAT_ORD
+#define SLAT_FR_FLAT_ORD 0
+#endif
 constexpr uint32_t kFlatHuge = 1u << 24;  // parts at least this long: walked by the whole wave alone
 // ORDERED (f64 in the reference's fold order): the wave walks every entry of the row itself, in A
 // order (each wave owns its own slice of the chunk's columns), and fn(c, a, b, valid) is called by the
@@ -520,12 +523,15 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
         const int lane = lane_id(), wv = threadIdx.x / kWave;
         const uint32_t g = g0 + (uint32_t)wv;
         if ((c0 + ((uint32_t)wv << f.gsh)) >= c1) return;
-        if constexpr (SLAT_FR_FLAT) {
-            // the wave's slice flattened over the row's entries (every lane on a product, whatever
-            // the parts' lengths), slots of 64 products in A order. Within a slot the lanes are in
-            // position order, so lanes on one column apply their products lowest lane first: the
-            // column's same-column lanes by one ballot per offset bit, then rounds by rank (one round
-            // unless two entries of the slot meet on a column)
+        if constexpr (SLAT_FR_FLAT_ORD) {
+            // (variant builds -DSLAT_FR_FLAT_ORD=1) the wave's slice flattened over the row's entries
+            // (every lane on a product, whatever the parts' lengths), slots of 64 products in A order.
+            // Within a slot the lanes are in position order, so lanes on one column apply their
+            // products lowest lane first: the column's same-column lanes by one ballot per offset bit,
+            // then rounds by rank (one round unless two entries of the slot meet on a column).
+            // Measured slower than the per-entry walk below (C5 2^16 fold 12.0 -> 13.0 ms, 2^18
+            // 96.0 -> 100.5, profiles/r04_ab6.txt): a wave slice gets ~0.4 products per A entry, so
+            // the per-64-entry loads and scans outweigh the idle lanes they save
             const uint32_t sw = 1u << f.gsh, s0 = c0 + ((uint32_t)wv << f.gsh);
             const uint64_t lt = (1ull << lane) - 1;
             fr_flat<S, true, I, true>(
