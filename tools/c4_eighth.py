@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Config C4 on one GPU: the whole product C = A^3 * A against one rank's share of an 8-way row
+split (slat_spgemm_rowblock over an eighth of the rows, the strong-scaling leg's per-rank call),
+synchronous device-resident calls, best of 3 means over 20 calls. Prints one JSON line."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sparse-linear-algebra-tests_amd"))
+import slat  # noqa: E402
+
+
+def timed(fn, calls=20, reps=3):
+    best = 1e30
+    for _ in range(reps):
+        slat.default_context(0).sync()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            c = fn()
+            del c
+        slat.default_context(0).sync()
+        best = min(best, (time.perf_counter() - t0) / calls * 1e3)
+    return best
+
+
+def main():
+    ctx = slat.default_context(0)
+    A = slat.torus_thinned_device(100, 3.0, slat.StdRng(), ctx)
+    P = A.matmul(A).matmul(A)
+    n = P.n
+    for _ in range(3):
+        P._spgemm(A)
+    full = timed(lambda: P._spgemm(A))
+    out = {"full_ms": round(full, 4)}
+    for k in (0, 3, 7):  # three of the eight blocks (equal row counts; a torus has uniform rows)
+        lo, hi = k * n // 8, (k + 1) * n // 8
+        ms = timed(lambda: P.matmul_rowblock(lo, hi, A))
+        out[f"block{k}_ms"] = round(ms, 4)
+    worst = max(v for k, v in out.items() if k.startswith("block"))
+    out["full_over_worst_block"] = round(full / worst, 2)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
