@@ -563,20 +563,45 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                 wl);
             return;
         }
-        for (I base = a0; base < a1; base += (I)kWave) {
+        // 64 entries at a time, the next groups' loads in flight under this group's products: the
+        // entries two groups ahead, the B parts (bounds + split) one group ahead
+        auto load_k = [&](I base, uint32_t &k, S &a) {
             const I i = base + (I)lane;
-            S a = S(0);
-            I bs = 0, be = 0;
+            k = kSent;
+            a = S(0);
             if (i < a1) {
-                const uint32_t k = p.a_col[i];
+                k = p.a_col[i];
                 a = av[i];
-                if (k < p.b_nrows) {
-                    const I r = (I)p.b_rp[k];
-                    const uint32_t *sp = f.split + (uint64_t)k * f.nch1 + g;
-                    bs = r + (I)sp[0];
-                    be = r + (I)sp[1];
-                }
             }
+        };
+        auto load_part = [&](uint32_t k, I &bs, I &be) {
+            bs = be = 0;
+            if (k < p.b_nrows) {
+                const I r = (I)p.b_rp[k];
+                const uint32_t *sp = f.split + (uint64_t)k * f.nch1 + g;
+                bs = r + (I)sp[0];
+                be = r + (I)sp[1];
+            }
+        };
+        uint32_t kA, kB;
+        S aA, aB;
+        I bsA, beA;
+        load_k(a0, kA, aA);
+        load_k(a0 + (I)kWave, kB, aB);
+        load_part(kA, bsA, beA);
+        for (I base = a0; base < a1; base += (I)kWave) {
+            const S a = aA;
+            const I bs = bsA, be = beA;
+            I bsB, beB;
+            load_part(kB, bsB, beB);
+            uint32_t kC;
+            S aC;
+            load_k(base + (I)(2 * kWave), kC, aC);
+            bsA = bsB;
+            beA = beB;
+            aA = aB;
+            kB = kC;
+            aB = aC;
             unsigned long long m = __ballot(bs != be);
             uint32_t cn = 0;
             S vn = S(0), an = S(0);
