@@ -698,10 +698,18 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                       g_progress.load(std::memory_order_relaxed) == 0 &&
                       (unsigned __int128)a_nnz_block * maxrow_b <= (1u << 18) &&
                       (A->max_row_nnz ? (unsigned __int128)A->max_row_nnz * maxrow_b < slat_fat_min(false) : maxrow_b <= 32);
+    // rows of at most slat_lane_cap() products: the whole call in one kernel, a row per lane
+    // (slat_lane.hip: C1, the 30^3 chain's A * A, 88 -> ~25 us). Tried when the bound max row(A) x
+    // max row(B) is <= 4 caps; a row past the cap sets the mapped overflow word and the call reruns
+    // through the pipeline. Column ids < 2^26 (the sort keys carry a 6-bit slot)
+    static const bool kNoLane = slat_ab_knob("SLAT_NO_LANE") != nullptr;
+    const bool lane = !kNoLane && !tiny && idx32 && wait_mode() == 0 && !ablate && ncols <= (1ull << 26) &&
+                      !(flags & (SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) && g_progress.load(std::memory_order_relaxed) == 0 &&
+                      A->max_row_nnz && (unsigned __int128)A->max_row_nnz * maxrow_b <= 4 * slat_lane_cap();
     static const bool kNoEll = slat_ab_knob("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
-                     !kNoEll && !tiny;  // 24-bit row index, 31-bit byte offsets in the kernels
+                     !kNoEll && !tiny && !lane;  // 24-bit row index, 31-bit byte offsets in the kernels
     // stored bitmaps (single-window launches): symbolic keeps each row's touched bitmap blocks for
     // numeric, n * ww words at most (only touched blocks are written), capped against free memory
     // free device memory: re-read when this context's pool grew or shrank, else every 1024 calls
@@ -713,7 +721,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
     static const bool kNoSbm = slat_ab_knob("SLAT_NO_SBM") != nullptr;
-    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny;
+    const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny &&
+                     !lane;
     // a workgroup per row (slat_group.hip): single-window launches with B in ELL form. Symbolic for
     // every value type; numeric for the semirings that add with atomics (f64 in the reference's fold
     // order keeps the ordered wave-per-row walk), reading symbolic's stored bitmaps
@@ -749,7 +758,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                              (unsigned __int128)A->max_row_nnz * (4 * ((maxrow_b + 3) / 4)) <= kHashT / 2;
     const bool short1 = !a.wide && ell && !tiny && !ablate && (dt != SLAT_F64 || f64any) &&
                         ((kShort1 && bound_short) || kShort1Any);
-    const bool hash = (asym.wide || short1) && !kNoHash;
+    const bool hash = (asym.wide || short1) && !kNoHash && !lane;
     if (hash) {
         if (asym.wide) a.ww = std::min<uint32_t>(a.ww, 1024);
         a.b_maxrow = asym.b_maxrow = (uint32_t)std::min<uint64_t>(maxrow_b, 0xFFFFFFFFull);
@@ -848,7 +857,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     static const bool kNoFat = slat_ab_knob("SLAT_NO_FAT") != nullptr;
     const uint64_t maxrow_a = A->max_row_nnz;
     const uint64_t fat_min = slat_fat_min(!ell && (dt != SLAT_F64 || f64any));
-    const bool fat = !kNoFat && !tiny && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= fat_min : maxrow_b > 32);
+    const bool fat = !kNoFat && !tiny && !lane && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= fat_min : maxrow_b > 32);
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
@@ -865,7 +874,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             a.b_vmax = ctx->d_vmax;
             a.epoch = ++ctx->epoch;
         }
-    } else if (dt != SLAT_F64 && kNarrowCsr && !tiny) {
+    } else if (dt != SLAT_F64 && kNarrowCsr && !tiny && !lane) {
         // B walked in CSR form: k_bvmax gives the numeric pass the same max(B) (narrow slots, and
         // hub rows accumulate in C instead of one re-traversal per rank chunk)
         a.b_vmax = ctx->d_vmax;
@@ -879,7 +888,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         a.nblk = a.ww / kWave;
     }
     a.host_out = ctx->h_out_dev;
-    ctx->h_out[0] = ctx->h_out[1] = ctx->h_out[2] = 0;  // no kernel of this context is in flight
+    ctx->h_out[0] = ctx->h_out[1] = ctx->h_out[2] = ctx->h_out[3] = 0;  // no kernel of this context is in flight
     hc.mark(2);
     // the ELL image (or B's value summary) first: it runs while the host allocates C and queues
     // the rest, instead of after the host's setup with the GPU idle
@@ -978,6 +987,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     hc.mark(4);
     hipError_t e;
     const bool run_tiny = tiny && !exact;
+    const bool run_lane = lane && !exact;
     if (run_tiny) {
         // the whole call in one kernel: a wave per row, every block resident (<= 1024 blocks of
         // <= 30 KB LDS), block offsets by look-back; it stores the completion word itself
@@ -992,6 +1002,28 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         hc.mark(5);
         hc.mark(6);
         SLAT_HIPC(wait_stream(ctx, s, a.seq));
+    } else if (run_lane) {
+        // the whole call in one kernel, a row per lane, a wave's 64 rows per block; block offsets by
+        // look-back; it stores the completion word itself (timing: the kernel is the "numeric" pass)
+        a.c_col = C->col_idx;
+        a.c_val = C->values;
+        a.seq = ++ctx->done_seq;
+        a.done = ctx->d_words + 6;
+        const uint64_t g = (n + kWave - 1) / kWave;
+        if ((st = ensure_status(ctx, g, s))) return failc(st);
+        const uint32_t epoch = slat_next_scan_epoch(ctx, s);
+        if (timing)
+            for (int i = 0; i < 3; ++i) SLAT_HIPC(hipEventRecord(ctx->ev[i], s));
+        SLAT_HIPC(slat_launch_lane(sem, dim3((unsigned)g), s, a, ctx->d_status, epoch, ctx->d_words + 2));
+        if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));
+        hc.mark(5);
+        hc.mark(6);
+        SLAT_HIPC(wait_stream(ctx, s, a.seq));
+        if (ctx->h_out[3]) {
+            // a row of more than slat_lane_cap() products: the call through the pipeline
+            (void)failc(SLAT_OK);
+            return slat_spgemm_rowblock(ctx, A, row_begin, row_end, B, C, flags | SLAT_FLAG_NO_TINY);
+        }
     } else {
     if (a.stats || SLAT_PHASES) SLAT_HIPC(hipMemsetAsync(a.shards, 0, shards_b, s));
     asym.counts = a.counts;
@@ -1224,7 +1256,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     S.nnz = nnz;
     S.flops = flops;
     S.capacity = C->capacity;
-    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u);
+    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u) | (run_lane ? 8u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;

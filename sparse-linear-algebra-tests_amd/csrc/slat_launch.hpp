@@ -69,3 +69,10 @@ hipError_t slat_launch_group_numeric(int gt, int sem, bool idx32, dim3 grid, siz
 size_t slat_group_numeric_lds(uint32_t ww, uint32_t area);
 // resident 256-thread blocks per CU of the symbolic (numeric = false) or numeric instance at `lds`
 int slat_group_blocks_per_cu(int gt, int sem, bool numeric, bool idx32, size_t lds, uint32_t ww);
+
+// rows of at most slat_lane_cap() products in one kernel, a row per lane (slat_lane.hip): n rows in
+// ceil(n / 64) one-wave blocks, status = look-back words (>= the block count), maxw = max-row word;
+// sets host_out[3] when a row has more products than the cap
+uint32_t slat_lane_cap();
+hipError_t slat_launch_lane(int sem, dim3 grid, hipStream_t s, const slat::Args &a, unsigned long long *status,
+                            uint32_t epoch, unsigned long long *maxw);

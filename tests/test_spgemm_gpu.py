@@ -484,3 +484,51 @@ def test_wide_csr_b_short_row_batches(ctx, dtype, vals):
         np.testing.assert_allclose(h.values, val, rtol=1e-12, atol=1e-12)
     else:
         assert_same(got, want, f"wide CSR-B short batches {vals}")
+
+
+@pytest.mark.parametrize("dtype", [slat.U32, slat.SAT64, slat.F64])
+@pytest.mark.parametrize("case", ["c1", "overflow", "zeros", "big", "wide"])
+def test_lane_rows(ctx, dtype, case):
+    """Products whose rows hold at most 64 products run as one kernel, a row per lane
+    (slat_lane.hip, mode bit 8): the 30^3 chain's A * A (C1) and its variants. overflow: a bound
+    that admits the kernel (max row(A) x max row(B) <= 256) but a row of 100 products, so the call
+    reruns through the pipeline; zeros: explicit zero values (zero sums dropped in-kernel); big:
+    products and sums past 2^32 (u32 saturates, Sat64 keeps them); wide: 70 000 columns. Every case
+    against the oracle and against the pipeline (SLAT_FLAG_NO_TINY)."""
+    rng = np.random.default_rng({"c1": 1, "overflow": 2, "zeros": 3, "big": 4, "wide": 5}[case])
+    if case == "c1":
+        h = slat.torus_thinned(30, 3.0, slat.StdRng())
+        rp = h.row_ptr.astype(np.int64)
+        rows = np.repeat(np.arange(h.n), np.diff(rp))
+        vals = rng.integers(1, 5, len(rows)) if dtype != slat.F64 else rng.standard_normal(len(rows))
+        a = O.from_coo(h.n, rows, h.col_idx.astype(np.int64), vals, DT[dtype])
+        b = a
+    else:
+        n = 70_000 if case == "wide" else 5000
+        lens = rng.integers(0, 6, n)
+        if case == "overflow":
+            lens[17] = 10  # 10 entries x B rows of 10 = 100 products > 64
+        ar = np.repeat(np.arange(n), lens)
+        ac = np.concatenate([rng.choice(n, k, replace=False) for k in lens])
+        bl = rng.integers(1, 7, n)
+        if case == "overflow":
+            bl[ac[lens[:17].sum():lens[:18].sum()]] = 10
+        br = np.repeat(np.arange(n), bl)
+        bc = np.concatenate([rng.choice(n, k, replace=False) for k in bl])
+        if dtype == slat.F64:
+            av, bv = rng.standard_normal(len(ar)), rng.standard_normal(len(br))
+            if case == "zeros":
+                bv[::4] = 0.0
+        else:
+            hi = (1 << 31) + 9 if case == "big" else 5
+            av = rng.integers(1, hi, len(ar))
+            bv = rng.integers(0 if case == "zeros" else 1, hi, len(br))
+        a = O.from_coo(n, ar, ac, av, DT[dtype])
+        b = O.from_coo(n, br, bc, bv, DT[dtype])
+    da, db = to_dev(a, dtype), to_dev(b, dtype)
+    want = O.matmul_seq(a, b)
+    got = da._spgemm(db)
+    if case != "overflow":
+        assert ctx.stats()["mode"] & 8, "the lane kernel did not run"
+    assert_same(got, want, f"lane rows {case}")
+    assert_same(da._spgemm(db, slat.FLAG_NO_TINY), want, f"pipeline {case}")
