@@ -1009,7 +1009,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         a.c_val = C->values;
         a.seq = ++ctx->done_seq;
         a.done = ctx->d_words + 6;
-        const uint64_t g = (n + kWave - 1) / kWave;
+        const uint64_t g = (n + slat_lane_rows() - 1) / slat_lane_rows();
         if ((st = ensure_status(ctx, g, s))) return failc(st);
         const uint32_t epoch = slat_next_scan_epoch(ctx, s);
         if (timing)

@@ -269,6 +269,9 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
 #ifndef SLAT_FR_FLAT_ORD
 #define SLAT_FR_FLAT_ORD 0
 #endif
+#ifndef SLAT_FOLD_PREFETCH
+#define SLAT_FOLD_PREFETCH 1
+#endif
 constexpr uint32_t kFlatHuge = 1u << 24;  // parts at least this long: walked by the whole wave alone
 // ORDERED (f64 in the reference's fold order): the wave walks every entry of the row itself, in A
 // order (each wave owns its own slice of the chunk's columns), and fn(c, a, b, valid) is called by the
@@ -564,7 +567,8 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
             return;
         }
         // 64 entries at a time, the next groups' loads in flight under this group's products: the
-        // entries two groups ahead, the B parts (bounds + split) one group ahead
+        // entries two groups ahead, the B parts (bounds + split) one group ahead (variant builds
+        // -DSLAT_FOLD_PREFETCH=0: each group's loads when it starts)
         auto load_k = [&](I base, uint32_t &k, S &a) {
             const I i = base + (I)lane;
             k = kSent;
@@ -590,26 +594,37 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
         load_k(a0 + (I)kWave, kB, aB);
         load_part(kA, bsA, beA);
         for (I base = a0; base < a1; base += (I)kWave) {
-            const S a = aA;
-            const I bs = bsA, be = beA;
+            S a_now = aA;
+            I bs_now = bsA, be_now = beA;
             I bsB, beB;
-            load_part(kB, bsB, beB);
             uint32_t kC;
             S aC;
-            load_k(base + (I)(2 * kWave), kC, aC);
+            if constexpr (SLAT_FOLD_PREFETCH) {
+                load_part(kB, bsB, beB);
+                load_k(base + (I)(2 * kWave), kC, aC);
+            } else {
+                bsB = beB = 0;
+                kC = kSent;
+                aC = S(0);
+            }
             bsA = bsB;
             beA = beB;
             aA = aB;
             kB = kC;
             aB = aC;
-            unsigned long long m = __ballot(bs != be);
+            if constexpr (!SLAT_FOLD_PREFETCH) {  // this group's loads now (the round-3 walk)
+                load_k(base, kA, aA);
+                a_now = aA;
+                load_part(kA, bs_now, be_now);
+            }
+            unsigned long long m = __ballot(bs_now != be_now);
             uint32_t cn = 0;
             S vn = S(0), an = S(0);
             I sn = 0, en = 0;
             auto fetch = [&](int t) {
-                sn = (I)readlane_u64((uint64_t)bs, t);
-                en = (I)readlane_u64((uint64_t)be, t);
-                an = readlane_val(a, t);
+                sn = (I)readlane_u64((uint64_t)bs_now, t);
+                en = (I)readlane_u64((uint64_t)be_now, t);
+                an = readlane_val(a_now, t);
                 if (sn + (I)lane < en) {
                     cn = p.b_col[sn + (I)lane];
                     vn = bv[sn + (I)lane];

@@ -11,7 +11,7 @@
 //      products' offset in the wave's flattened product space (a wave prefix);
 //   2. the products are walked flattened, 256 per pass, every lane on one (an entry by markers, as
 //      the fat rows' fr_flat) and written into their row's lane of an LDS slot table (slot s of row l
-//      at s * 64 + l) as (column << 6 | slot, product): the slot is the product's position in the
+//      at s * rows + l) as (column << 6 | slot, product): the slot is the product's position in the
 //      row, A order then B order, so the key is unique and keeps the reference's order for equal
 //      columns;
 //   3. every lane sorts its row's slots in registers (a bitonic network of 16, 32 or 64 keys, the
@@ -36,14 +36,18 @@ using namespace slat;
 namespace {
 
 constexpr uint32_t kLaneCap = 64;   // products per row (sort slots per lane)
+#ifndef SLAT_LANE_ROWS
+#define SLAT_LANE_ROWS 64
+#endif
+constexpr uint32_t kLaneRows = SLAT_LANE_ROWS;  // rows per one-wave block (variant builds: 32)
 constexpr uint32_t kLaneSeg = 256;  // A entries / products per pass (four per lane)
 
 template <typename S>
 __host__ __device__ constexpr size_t lane_lds() {
-    // slot keys u32[64 * 64] | slot values S[64 * 64] | entry bases u32[256] | entry A values S[256] |
+    // slot keys u32[64 * rows] | slot values S[64 * rows] | entry bases u32[256] | entry A values S[256] |
     // entry rows u8[256] | entry markers u8[256] | product markers u16[256] | row bases u32[64] |
     // row counts u32[64]
-    return (size_t)kLaneCap * kWave * (4 + sizeof(S)) + kLaneSeg * (4 + sizeof(S) + 1 + 1 + 2) + kWave * 8;
+    return (size_t)kLaneCap * kLaneRows * (4 + sizeof(S)) + kLaneSeg * (4 + sizeof(S) + 1 + 1 + 2) + kWave * 8;
 }
 
 // the semiring's running sum of one output
@@ -131,8 +135,8 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
     using S = typename Sem::S;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t *skey = (uint32_t *)smem;
-    S *sval = (S *)(smem + kLaneCap * kWave * 4);
-    uint8_t *q = smem + kLaneCap * kWave * (4 + sizeof(S));
+    S *sval = (S *)(smem + kLaneCap * kLaneRows * 4);
+    uint8_t *q = smem + kLaneCap * kLaneRows * (4 + sizeof(S));
     uint32_t *eb = (uint32_t *)q;
     S *ea = (S *)(q + kLaneSeg * 4);
     uint8_t *erl = q + kLaneSeg * (4 + sizeof(S));
@@ -145,8 +149,8 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
     const auto plus = [](uint32_t x, uint32_t y) { return x + y; };
     const auto mx = [](uint32_t x, uint32_t y) { return max(x, y); };
 
-    const uint64_t r0 = (uint64_t)blockIdx.x * kWave, r = r0 + lane;
-    const uint32_t nt = (uint32_t)min<uint64_t>(kWave, p.nrows - r0);
+    const uint64_t r0 = (uint64_t)blockIdx.x * kLaneRows, r = r0 + lane;
+    const uint32_t nt = (uint32_t)min<uint64_t>(kLaneRows, p.nrows - r0);
     uint32_t A0j = 0, A1j = 0;
     if (lane < nt) {
         A0j = (uint32_t)p.a_rp[r];
@@ -242,8 +246,8 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
             });
             sfor<4>([&](auto Q) {
                 if (c[Q] != kSent && slot[Q] < kLaneCap) {
-                    skey[slot[Q] * kWave + row[Q]] = (c[Q] << 6) | slot[Q];
-                    sval[slot[Q] * kWave + row[Q]] = Sem::prod(a[Q], v[Q]);
+                    skey[slot[Q] * kLaneRows + row[Q]] = (c[Q] << 6) | slot[Q];
+                    sval[slot[Q] * kLaneRows + row[Q]] = Sem::prod(a[Q], v[Q]);
                 }
             });
             wave_sync();
@@ -269,8 +273,8 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
             k[s] = kSent;
             v[s] = S(0);
             if ((uint32_t)s < cn) {
-                k[s] = skey[s * kWave + lane];
-                v[s] = sval[s * kWave + lane];
+                k[s] = skey[s * kLaneRows + lane];
+                v[s] = sval[s * kLaneRows + lane];
             }
         }
         lane_sort<N>(k, v);
@@ -333,6 +337,7 @@ hipError_t launch(dim3 grid, hipStream_t s, const Args &a, unsigned long long *s
 }  // namespace
 
 uint32_t slat_lane_cap() { return kLaneCap; }
+uint32_t slat_lane_rows() { return kLaneRows; }
 
 hipError_t slat_launch_lane(int sem, dim3 grid, hipStream_t s, const Args &a, unsigned long long *status,
                             uint32_t epoch, unsigned long long *maxw) {

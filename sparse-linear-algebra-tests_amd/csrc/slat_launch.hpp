@@ -74,5 +74,6 @@ int slat_group_blocks_per_cu(int gt, int sem, bool numeric, bool idx32, size_t l
 // ceil(n / 64) one-wave blocks, status = look-back words (>= the block count), maxw = max-row word;
 // sets host_out[3] when a row has more products than the cap
 uint32_t slat_lane_cap();
+uint32_t slat_lane_rows();  // rows per block
 hipError_t slat_launch_lane(int sem, dim3 grid, hipStream_t s, const slat::Args &a, unsigned long long *status,
                             uint32_t epoch, unsigned long long *maxw);
