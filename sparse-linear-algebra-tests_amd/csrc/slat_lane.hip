@@ -14,8 +14,9 @@
 //      at s * rows + l) as (column << 6 | slot, product): the slot is the product's position in the
 //      row, A order then B order, so the key is unique and keeps the reference's order for equal
 //      columns;
-//   3. every lane sorts its row's slots in registers (a bitonic network of 16, 32 or 64 keys, the
-//      wave's longest row decides), sums equal columns in key order — the f64 left fold from 0.0 in A
+//   3. every lane sorts its row's keys in registers (a bitonic network of 16, 32 or 64 keys, the
+//      wave's longest row decides; the values stay in LDS, found by the slot in the key), sums equal
+//      columns in key order — the f64 left fold from 0.0 in A
 //      order, the saturating integer sums — and counts the non-zero results (zero sums are dropped, as
 //      matmul does, so there is nothing to compact);
 //   4. the wave's offset by a decoupled look-back over the earlier waves' status words (one wave per
@@ -77,9 +78,11 @@ struct LaneSum {
     }
 };
 
-// ascending bitonic sort of N (key, value) pairs held by the lane (compile-time indices only)
-template <int N, typename T>
-__device__ __forceinline__ void lane_sort(uint32_t (&k)[kLaneCap], T (&v)[kLaneCap]) {
+// ascending bitonic sort of the lane's N keys (compile-time indices only). The keys are unique
+// (column << 6 | slot) and carry their slot, so no payload moves: each compare-exchange is one min
+// and one max
+template <int N>
+__device__ __forceinline__ void lane_sort(uint32_t (&k)[kLaneCap]) {
 #pragma unroll
     for (int size = 2; size <= N; size <<= 1)
 #pragma unroll
@@ -88,38 +91,34 @@ __device__ __forceinline__ void lane_sort(uint32_t (&k)[kLaneCap], T (&v)[kLaneC
             for (int i = 0; i < N; ++i) {
                 const int j = i ^ stride;
                 if (j > i) {
+                    const uint32_t lo = min(k[i], k[j]), hi = max(k[i], k[j]);
                     const bool asc = (i & size) == 0;
-                    const bool sw = asc ? k[i] > k[j] : k[i] < k[j];
-                    const uint32_t ki = k[i];
-                    const T vi = v[i];
-                    k[i] = sw ? k[j] : ki;
-                    k[j] = sw ? ki : k[j];
-                    v[i] = sw ? v[j] : vi;
-                    v[j] = sw ? vi : v[j];
+                    k[i] = asc ? lo : hi;
+                    k[j] = asc ? hi : lo;
                 }
             }
 }
 
-// the lane's sorted slots: emit(col, value, index) for each non-zero sum in column order; returns
-// the number of them
+// the lane's sorted keys: emit(col, value, index) for each non-zero sum in column order (values by
+// slot from the lane's column of the slot table); returns the number of them
 template <typename Sem, int N, typename F>
-__device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], const typename Sem::S (&v)[kLaneCap],
-                                                 F &&emit) {
+__device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], const typename Sem::S *sv, F &&emit) {
     using L = LaneSum<Sem>;
     typename L::T s{};
     uint32_t prev = kSent, nz = 0;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const uint32_t c = k[i] == kSent ? kSent : k[i] >> 6;
+        const typename Sem::S v = c == kSent ? typename Sem::S(0) : sv[(k[i] & 63u) * kLaneRows];
         if (c != prev) {
             if (prev != kSent) {
                 const auto out = L::done(s);
                 if (!Sem::is_zero(out)) emit(prev, out, nz++);
             }
-            if (c != kSent) s = L::first(v[i]);
+            if (c != kSent) s = L::first(v);
             prev = c;
         } else if (c != kSent) {
-            s = L::add(s, v[i]);
+            s = L::add(s, v);
         }
     }
     if (prev != kSent) {
@@ -267,18 +266,11 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
     auto body = [&](auto ntag) {
         constexpr int N = decltype(ntag)::value;
         uint32_t k[kLaneCap];
-        S v[kLaneCap];
 #pragma unroll
-        for (int s = 0; s < N; ++s) {
-            k[s] = kSent;
-            v[s] = S(0);
-            if ((uint32_t)s < cn) {
-                k[s] = skey[s * kLaneRows + lane];
-                v[s] = sval[s * kLaneRows + lane];
-            }
-        }
-        lane_sort<N>(k, v);
-        const uint32_t nz = lane_combine<Sem, N>(k, v, [](uint32_t, S, uint32_t) {});
+        for (int s = 0; s < N; ++s) k[s] = (uint32_t)s < cn ? skey[s * kLaneRows + lane] : kSent;
+        lane_sort<N>(k);
+        const S *sv = sval + lane;  // slot s of this lane's row at sv[s * kLaneRows]
+        const uint32_t nz = lane_combine<Sem, N>(k, sv, [](uint32_t, S, uint32_t) {});
         // 4. the wave's offset (look-back over the earlier blocks), row_ptr, the rows' outputs
         const uint32_t incl = wave_incl_scan(nz, 0u, plus);
         const uint32_t agg = readlane_u32(incl, kWave - 1);
@@ -306,7 +298,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         if (nz) {
             uint32_t *oc = p.c_col + base;
             S *ov = (S *)p.c_val + base;
-            (void)lane_combine<Sem, N>(k, v, [&](uint32_t col, S val, uint32_t j) {
+            (void)lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
                 oc[j] = col;
                 ov[j] = val;
             });
