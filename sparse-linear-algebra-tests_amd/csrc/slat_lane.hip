@@ -20,7 +20,7 @@
 //      order, the saturating integer sums — and counts the non-zero results (zero sums are dropped, as
 //      matmul does, so there is nothing to compact);
 //   4. the wave's offset by a decoupled look-back over the earlier waves' status words (one wave per
-//      block, lookback_prefix), then row_ptr and the rows' outputs are stored; the last block stores
+//      block; lookback_prefix_wave reads 64 predecessors per round), then row_ptr and the rows' outputs are stored; the last block stores
 //      nnz, the max row and the completion word.
 //
 // A row of more than kLaneCap products sets the mapped overflow word: the host then runs the call
@@ -260,7 +260,6 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         __hip_atomic_store(&p.host_out[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t cn = cnt > kLaneCap ? 0u : cnt;
     const uint32_t wmax = wave_max_u32(cn);
-    __shared__ unsigned long long s_pre;
     // sorted once (network size by the wave's longest row); the non-zero count first, then the
     // wave's offset, then the outputs from the same registers
     auto body = [&](auto ntag) {
@@ -275,10 +274,11 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         const uint32_t incl = wave_incl_scan(nz, 0u, plus);
         const uint32_t agg = readlane_u32(incl, kWave - 1);
         const uint32_t rmax = wave_max_u32(nz);
+        // (the max row first, its result waited for: it is in place once a later block sees this
+        // block's status, so the last block reads the final max after its look-back)
+        if (lane == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | rmax));
+        const unsigned long long excl = lookback_prefix_wave(status, blockIdx.x, epoch, agg);
         if (lane == 0) {
-            pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | rmax));
-            const unsigned long long excl = lookback_prefix(status, blockIdx.x, epoch, agg);
-            s_pre = excl;
             if (blockIdx.x == gridDim.x - 1) {
                 const unsigned long long mw = __hip_atomic_load(maxw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long mxr = (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull;
@@ -289,8 +289,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
                 asm volatile("" ::"v"(o0), "v"(o1));
             }
         }
-        wave_sync();
-        const uint64_t base = s_pre + (incl - nz);
+        const uint64_t base = excl + (incl - nz);
         if (lane < nt) {
             p.c_rp[r + 1] = base + nz;
             if (r == 0) p.c_rp[0] = 0;

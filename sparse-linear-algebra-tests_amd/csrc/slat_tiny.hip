@@ -7,7 +7,8 @@
 //   1. the row's column bitmap and word ranks in LDS (numeric's steps 1-2: B walked in CSR form, no
 //      ELL image to build); the rank total IS the row's structural count;
 //   2. the block's counts summed in LDS, then the block's offset by a decoupled look-back over the
-//      earlier blocks' epoch-tagged status words (lookback_prefix, as k_scan_rows' tiles) — no grid
+//      earlier blocks' epoch-tagged status words (lookback_prefix_wave: the first wave reads 64
+//      predecessors per round) — no grid
 //      barrier, no cooperative launch: a block only ever waits on lower-numbered blocks, which the
 //      hardware dispatched before it;
 //   3. row_ptr[row + 1] stored, then the row's values accumulated in rank slots and emitted sorted
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(kBlock) void k_tiny(Args p, unsigned long long *sta
     // 2. the block's offset: its aggregate published, the earlier blocks' looked back over
     if (lane == 0) s_cnt[wv] = wcnt;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kWave) {  // the first wave: the look-back reads 64 predecessors per round
         unsigned long long agg = 0;
         uint32_t mx = 0;
 #pragma unroll
@@ -87,10 +88,10 @@ __global__ __launch_bounds__(kBlock) void k_tiny(Args p, unsigned long long *sta
         }
         // the max row first (its result waited for): it is in place once a later block sees this
         // block's status, so the last block reads the final max after its look-back
-        pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | mx));
-        const unsigned long long excl = lookback_prefix(status, blockIdx.x, epoch, agg);
-        s_pre = excl;
-        if (blockIdx.x == gridDim.x - 1) {
+        if (threadIdx.x == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | mx));
+        const unsigned long long excl = lookback_prefix_wave(status, blockIdx.x, epoch, agg);
+        if (threadIdx.x == 0) s_pre = excl;
+        if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) {
             const unsigned long long mw = __hip_atomic_load(maxw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long mxr = (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull;
             // returned values: both words have landed before this block reports done (signal_done)

@@ -2728,6 +2728,50 @@ __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long l
     return v;
 }
 
+// The same protocol by a whole wave: lane j reads tile - 1 - j, so one round covers 64 predecessors
+// (the nearest inclusive prefix by ballot, the aggregates before it by a wave sum) instead of one
+// dependent load per predecessor. Many small tiles arriving together (k_lane: ~400 one-wave blocks)
+// made the lane-0 walk a chain of hundreds of loads. Called by every lane of the wave; returns the
+// tile's exclusive prefix in every lane.
+__device__ __forceinline__ unsigned long long lookback_prefix_wave(unsigned long long *status, uint64_t tile,
+                                                                   uint32_t epoch, unsigned long long agg) {
+    auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto st = [](unsigned long long *x, unsigned long long v) {
+        __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    const int lane = lane_id();
+    const unsigned long long tag = (unsigned long long)epoch << 42;
+    if (tile == 0) {
+        if (lane == 0) st(&status[0], tag | kStInc | agg);
+        return 0;
+    }
+    if (lane == 0) st(&status[tile], tag | kStAgg | agg);
+    unsigned long long excl = 0;
+    for (int64_t j0 = (int64_t)tile - 1;; j0 -= kWave) {
+        const int64_t j = j0 - lane;
+        unsigned long long x = 0;
+        while (true) {
+            bool ok = true;
+            if (j >= 0) {
+                x = ld(&status[j]);
+                ok = (x >> 42) == epoch && (x & (kStAgg | kStInc)) != 0;
+            }
+            if (__ballot(!ok) == 0) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const unsigned long long inc = __ballot(j >= 0 && (x & kStInc));
+        // lanes up to the nearest inclusive prefix (all 64 when there is none in this round)
+        const int last = inc ? (int)__builtin_ctzll(inc) : kWave - 1;
+        unsigned long long v = (j >= 0 && lane <= last) ? (x & kStVal) : 0ull;
+        v = wave_incl_scan_u64(v);
+        excl += readlane_u64(v, kWave - 1);
+        if (inc) break;
+    }
+    if (lane == 0) st(&status[tile], tag | kStInc | (excl + agg));
+    return excl;
+}
+
+
 // bpart (optional): k_build_ell's nbpart per-block B-value partials ((~min << 32) | max), reduced by
 // one wave of tile 0 into vmax[kVMaxWord] = (vepoch << 32) | max, vmax[kVMinInvWord] =
 // (vepoch << 32) | ~min for the numeric pass (which runs after this kernel)
