@@ -1014,6 +1014,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         const uint32_t epoch = slat_next_scan_epoch(ctx, s);
         if (timing)
             for (int i = 0; i < 3; ++i) SLAT_HIPC(hipEventRecord(ctx->ev[i], s));
+        if (SLAT_PHASES) SLAT_HIPC(hipMemsetAsync(a.shards, 0, shards_b, s));
         SLAT_HIPC(slat_launch_lane(sem, dim3((unsigned)g), s, a, ctx->d_status, epoch, ctx->d_words + 2));
         if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));
         hc.mark(5);

@@ -148,6 +148,8 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
     const auto plus = [](uint32_t x, uint32_t y) { return x + y; };
     const auto mx = [](uint32_t x, uint32_t y) { return max(x, y); };
 
+    PhaseClock pc{};  // diagnostic builds (SLAT_PHASES): where a wave's time goes
+    if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
     const uint64_t r0 = (uint64_t)blockIdx.x * kLaneRows, r = r0 + lane;
     const uint32_t nt = (uint32_t)min<uint64_t>(kLaneRows, p.nrows - r0);
     uint32_t A0j = 0, A1j = 0;
@@ -162,6 +164,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
     rbase[lane] = 0;
     wave_sync();
 
+    pc.mark(0);  // row bounds, LDS init
     // 1-2. entries 256 at a time, then their products flattened
     uint32_t rcarry = 0, fcarry = 0;  // row lane (+1) running into the segment, flat products so far
     for (uint32_t sb = A0; sb < A1; sb += kLaneSeg) {
@@ -211,6 +214,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
             erl[e] = (uint8_t)rl[Q];
         });
         wave_sync();
+        pc.mark(1);  // entries: rows, B row bounds, offsets
         // the segment's products, 256 per pass: entry by markers, slot = t - the row's base
         for (uint32_t p0 = 0; p0 < stot; p0 += kLaneSeg) {
             const uint32_t t0 = fcarry + p0;
@@ -252,6 +256,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
             wave_sync();
         }
         fcarry += stot;
+        pc.mark(2);  // products into the slot table
     }
 
     // 3. the lane's row: its slots sorted in registers, equal columns summed
@@ -267,9 +272,12 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         uint32_t k[kLaneCap];
 #pragma unroll
         for (int s = 0; s < N; ++s) k[s] = (uint32_t)s < cn ? skey[s * kLaneRows + lane] : kSent;
+        pc.mark(3);
         lane_sort<N>(k);
+        pc.mark(4);  // the sort
         const S *sv = sval + lane;  // slot s of this lane's row at sv[s * kLaneRows]
         const uint32_t nz = lane_combine<Sem, N>(k, sv, [](uint32_t, S, uint32_t) {});
+        pc.mark(5);  // the count pass
         // 4. the wave's offset (look-back over the earlier blocks), row_ptr, the rows' outputs
         const uint32_t incl = wave_incl_scan(nz, 0u, plus);
         const uint32_t agg = readlane_u32(incl, kWave - 1);
@@ -289,6 +297,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
                 asm volatile("" ::"v"(o0), "v"(o1));
             }
         }
+        pc.mark(6);  // look-back
         const uint64_t base = excl + (incl - nz);
         if (lane < nt) {
             p.c_rp[r + 1] = base + nz;
@@ -302,6 +311,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
                 ov[j] = val;
             });
         }
+        pc.mark(7);  // row_ptr, the emit
     };
     if (wmax <= 16)
         body(std::integral_constant<int, 16>{});
@@ -309,6 +319,13 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         body(std::integral_constant<int, 32>{});
     else
         body(std::integral_constant<int, 64>{});
+    if constexpr (SLAT_PHASES) {
+        pc.ph[kPhaseSlots - 1] = 1;  // waves
+        if (lane == 0) {
+            unsigned long long *dst = p.shards + 512 + (blockIdx.x % 64) * kPhaseSlots;
+            for (int i = 0; i < kPhaseSlots; ++i) atomicAdd(&dst[i], (unsigned long long)pc.ph[i]);
+        }
+    }
     signal_done(p);
 }
 
