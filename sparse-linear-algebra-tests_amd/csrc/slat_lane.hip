@@ -15,12 +15,13 @@
 //      row, A order then B order, so the key is unique and keeps the reference's order for equal
 //      columns;
 //   3. every lane sorts its row's keys in registers (a bitonic network of 16, 32 or 64 keys, the
-//      wave's longest row decides; the values stay in LDS, found by the slot in the key), sums equal
-//      columns in key order — the f64 left fold from 0.0 in A
-//      order, the saturating integer sums — and counts the non-zero results (zero sums are dropped, as
-//      matmul does, so there is nothing to compact);
+//      wave's longest row decides; the values stay in LDS, found by the slot in the key) and counts
+//      its distinct columns;
 //   4. the wave's offset by a decoupled look-back over the earlier waves' status words (one wave per
-//      block; lookback_prefix_wave reads 64 predecessors per round), then row_ptr and the rows' outputs are stored; the last block stores
+//      block; lookback_prefix_wave reads 64 predecessors per round), then row_ptr, and the rows'
+//      sums in key order — the f64 left fold from 0.0 in A order, the saturating integer sums — are
+//      stored; zero sums (explicit zero inputs, f64 cancellation) are counted for the host's
+//      compaction, as after k_numeric. The last block stores
 //      nnz, the max row and the completion word.
 //
 // A row of more than kLaneCap products sets the mapped overflow word: the host then runs the call
@@ -99,13 +100,23 @@ __device__ __forceinline__ void lane_sort(uint32_t (&k)[kLaneCap]) {
             }
 }
 
-// the lane's sorted keys: emit(col, value, index) for each non-zero sum in column order (values by
-// slot from the lane's column of the slot table); returns the number of them
+// the lane's sorted keys: distinct columns (the row's structural count; no values read)
+template <int N>
+__device__ __forceinline__ uint32_t lane_count(const uint32_t (&k)[kLaneCap]) {
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        nz += (k[i] != kSent && (i == 0 || (k[i] >> 6) != (k[i - 1] >> 6))) ? 1u : 0u;
+    return nz;
+}
+
+// the lane's sorted keys: emit(col, value, index) for each column's sum in column order (values by
+// slot from the lane's column of the slot table); returns the number of zero sums among them
 template <typename Sem, int N, typename F>
 __device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], const typename Sem::S *sv, F &&emit) {
     using L = LaneSum<Sem>;
     typename L::T s{};
-    uint32_t prev = kSent, nz = 0;
+    uint32_t prev = kSent, j = 0, zeros = 0;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const uint32_t c = k[i] == kSent ? kSent : k[i] >> 6;
@@ -113,7 +124,8 @@ __device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], 
         if (c != prev) {
             if (prev != kSent) {
                 const auto out = L::done(s);
-                if (!Sem::is_zero(out)) emit(prev, out, nz++);
+                zeros += Sem::is_zero(out) ? 1u : 0u;
+                emit(prev, out, j++);
             }
             if (c != kSent) s = L::first(v);
             prev = c;
@@ -123,9 +135,10 @@ __device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], 
     }
     if (prev != kSent) {
         const auto out = L::done(s);
-        if (!Sem::is_zero(out)) emit(prev, out, nz++);
+        zeros += Sem::is_zero(out) ? 1u : 0u;
+        emit(prev, out, j++);
     }
-    return nz;
+    return zeros;
 }
 
 template <typename Sem>
@@ -276,7 +289,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         lane_sort<N>(k);
         pc.mark(4);  // the sort
         const S *sv = sval + lane;  // slot s of this lane's row at sv[s * kLaneRows]
-        const uint32_t nz = lane_combine<Sem, N>(k, sv, [](uint32_t, S, uint32_t) {});
+        const uint32_t nz = lane_count<N>(k);  // structural: zero sums are dropped afterwards
         pc.mark(5);  // the count pass
         // 4. the wave's offset (look-back over the earlier blocks), row_ptr, the rows' outputs
         const uint32_t incl = wave_incl_scan(nz, 0u, plus);
@@ -303,14 +316,20 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
             p.c_rp[r + 1] = base + nz;
             if (r == 0) p.c_rp[0] = 0;
         }
+        uint32_t zeros = 0;
         if (nz) {
             uint32_t *oc = p.c_col + base;
             S *ov = (S *)p.c_val + base;
-            (void)lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
+            zeros = lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
                 oc[j] = col;
                 ov[j] = val;
             });
         }
+        // zero sums (explicit zero inputs, f64 cancellation) stay in C for now: the row's non-zero
+        // count goes to p.counts and the rows with zeros to host_out[2], and the host compacts
+        // (as after k_numeric)
+        if (lane < nt) p.counts[r] = nz - zeros;
+        add_zero_rows(&p.host_out[2], wave_sum_u32(zeros ? 1u : 0u), true);
         pc.mark(7);  // row_ptr, the emit
     };
     if (wmax <= 16)
