@@ -2728,11 +2728,10 @@ __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long l
     return v;
 }
 
-// The same protocol by a whole wave: each round reads the 256 nearest unread predecessors, four per
-// lane (lane l, window w: tile - 1 - l - 64 w), finds the nearest inclusive prefix among them by
-// ballots and sums everything before it with DPP reductions (no LDS round trips). Many small tiles
-// arriving together (k_lane: ~400 one-wave blocks) made the lane-0 walk, one dependent load per
-// predecessor, the longest part of the kernel. Called by every lane of the wave; returns the
+// The same protocol by a whole wave: lane j reads tile - 1 - j, so one round covers 64 predecessors
+// (the nearest inclusive prefix by ballot, the aggregates before it by a wave sum) instead of one
+// dependent load per predecessor. Many small tiles arriving together (k_lane: ~400 one-wave blocks)
+// made the lane-0 walk a chain of hundreds of loads. Called by every lane of the wave; returns the
 // tile's exclusive prefix in every lane.
 __device__ __forceinline__ unsigned long long lookback_prefix_wave(unsigned long long *status, uint64_t tile,
                                                                    uint32_t epoch, unsigned long long agg) {
@@ -2740,7 +2739,6 @@ __device__ __forceinline__ unsigned long long lookback_prefix_wave(unsigned long
     auto st = [](unsigned long long *x, unsigned long long v) {
         __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    constexpr int kW = 4;
     const int lane = lane_id();
     const unsigned long long tag = (unsigned long long)epoch << 42;
     if (tile == 0) {
@@ -2749,39 +2747,25 @@ __device__ __forceinline__ unsigned long long lookback_prefix_wave(unsigned long
     }
     if (lane == 0) st(&status[tile], tag | kStAgg | agg);
     unsigned long long excl = 0;
-    for (int64_t j0 = (int64_t)tile - 1;; j0 -= kW * kWave) {
-        unsigned long long x[kW];
+    for (int64_t j0 = (int64_t)tile - 1;; j0 -= kWave) {
+        const int64_t j = j0 - lane;
+        unsigned long long x = 0;
         while (true) {
             bool ok = true;
-#pragma unroll
-            for (int w = 0; w < kW; ++w) {
-                const int64_t j = j0 - lane - (int64_t)w * kWave;
-                x[w] = 0;
-                if (j >= 0) {
-                    x[w] = ld(&status[j]);
-                    ok = ok && (x[w] >> 42) == epoch && (x[w] & (kStAgg | kStInc)) != 0;
-                }
+            if (j >= 0) {
+                x = ld(&status[j]);
+                ok = (x >> 42) == epoch && (x & (kStAgg | kStInc)) != 0;
             }
             if (__ballot(!ok) == 0) break;
             __builtin_amdgcn_s_sleep(1);
         }
-        // the nearest inclusive prefix: the first window with one, its lowest lane
-        int wi = kW, li = 0;
-#pragma unroll
-        for (int w = kW - 1; w >= 0; --w) {
-            const unsigned long long inc = __ballot((x[w] & kStInc) != 0);
-            if (inc) {
-                wi = w;
-                li = (int)__builtin_ctzll(inc);
-            }
-        }
-        unsigned long long v = 0;  // this lane's part of the sum (< 2^42)
-#pragma unroll
-        for (int w = 0; w < kW; ++w)
-            if (w < wi || (w == wi && lane <= li)) v += x[w] & kStVal;
-        const uint32_t lo = wave_sum_u32((uint32_t)(v & 0xFFFFFFu)), hi = wave_sum_u32((uint32_t)(v >> 24));
-        excl += (unsigned long long)lo + ((unsigned long long)hi << 24);
-        if (wi < kW) break;
+        const unsigned long long inc = __ballot(j >= 0 && (x & kStInc));
+        // lanes up to the nearest inclusive prefix (all 64 when there is none in this round)
+        const int last = inc ? (int)__builtin_ctzll(inc) : kWave - 1;
+        unsigned long long v = (j >= 0 && lane <= last) ? (x & kStVal) : 0ull;
+        v = wave_incl_scan_u64(v);
+        excl += readlane_u64(v, kWave - 1);
+        if (inc) break;
     }
     if (lane == 0) st(&status[tile], tag | kStInc | (excl + agg));
     return excl;
