@@ -789,15 +789,16 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         uint32_t cb = 1;
         while (cb < 64 && ((ncols - 1) >> cb)) ++cb;
         a.cbits = cb <= 25 ? cb : 0;
+        static const uint32_t kTileRows = [] {  // A/B knob: rows per tile (8 .. 64)
+            const char *e = slat_ab_knob("SLAT_TILE_ROWS");
+            return e ? (uint32_t)std::min(64, std::max(8, std::atoi(e))) : 0u;
+        }();
+        if (asym.wide && kTileRows) a.tile_rows = asym.tile_rows = kTileRows;
         if (!asym.wide) {
             a.sym_cap = asym.sym_cap = kHashT / 2;  // every counted row fits numeric's table
             // tiles of fewer rows when 64-row tiles would leave most resident waves idle (27 000 rows:
             // 422 tiles for ~6 000 waves): about 4 tiles per CU slot of 16 waves
             const uint64_t t = (n + (uint64_t)ctx->cu_count * 16 - 1) / ((uint64_t)ctx->cu_count * 16);
-            static const uint32_t kTileRows = [] {  // A/B knob: rows per tile (8 .. 64)
-                const char *e = slat_ab_knob("SLAT_TILE_ROWS");
-                return e ? (uint32_t)std::min(64, std::max(8, std::atoi(e))) : 0u;
-            }();
             a.tile_rows = asym.tile_rows = kTileRows ? kTileRows : (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, t));
         }
     }
