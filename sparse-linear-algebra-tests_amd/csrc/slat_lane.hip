@@ -49,7 +49,10 @@ __host__ __device__ constexpr size_t lane_lds() {
     // slot keys u32[64 * rows] | slot values S[64 * rows] | entry bases u32[256] | entry A values S[256] |
     // entry rows u8[256] | entry markers u8[256] | product markers u16[256] | row bases u32[64] |
     // row counts u32[64]
-    return (size_t)kLaneCap * kLaneRows * (4 + sizeof(S)) + kLaneSeg * (4 + sizeof(S) + 1 + 1 + 2) + kWave * 8;
+    // (+ u32 values: an output-value staging area u32[64 * rows], so the wave's outputs are stored
+    // coalesced; the columns stage in the slot keys' area, free once the keys are in registers)
+    return (size_t)kLaneCap * kLaneRows * (4 + sizeof(S)) + kLaneSeg * (4 + sizeof(S) + 1 + 1 + 2) + kWave * 8 +
+           (sizeof(S) == 4 ? (size_t)kLaneCap * kLaneRows * 4 : 0);
 }
 
 // the semiring's running sum of one output
@@ -155,6 +158,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
     uint8_t *amk = erl + kLaneSeg;
     uint16_t *pmk = (uint16_t *)(amk + kLaneSeg);
     uint32_t *rbase = (uint32_t *)(pmk + kLaneSeg), *rcnt = rbase + kWave;
+    S *stg = (S *)(rcnt + kWave);  // (u32 values) the outputs' value staging
     const uint32_t lane = (uint32_t)lane_id();
     const S *av = (const S *)p.a_val;
     const S *bv = (const S *)p.b_val;
@@ -317,7 +321,23 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
             if (r == 0) p.c_rp[0] = 0;
         }
         uint32_t zeros = 0;
-        if (nz) {
+        if constexpr (sizeof(S) == 4) {
+            // the wave's rows are contiguous in C: outputs staged in LDS at their wave offset, then
+            // stored coalesced (the scattered per-lane stores cost one instruction per output)
+            const uint32_t o0 = incl - nz;
+            if (nz)
+                zeros = lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
+                    skey[o0 + j] = col;
+                    stg[o0 + j] = val;
+                });
+            wave_sync();
+            uint32_t *oc = p.c_col + excl;
+            S *ov = (S *)p.c_val + excl;
+            for (uint32_t u = lane; u < agg; u += kWave) {
+                oc[u] = skey[u];
+                ov[u] = stg[u];
+            }
+        } else if (nz) {
             uint32_t *oc = p.c_col + base;
             S *ov = (S *)p.c_val + base;
             zeros = lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
