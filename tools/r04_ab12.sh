@@ -8,3 +8,8 @@ timeout -k 10 300 python -u -m pytest tests/test_spgemm_gpu.py -k "lane or golde
 tail -n 1 $OUT/pytest.log
 timeout -k 10 700 python tools/ab.py --reps 2 --steps 100 --chain --c4 k16 k17 k17:SLAT_TILE_ROWS=32 k17:SLAT_TILE_ROWS=16 > $OUT/ab.txt 2>&1 || { tail -30 $OUT/ab.txt; exit 1; }
 grep -A5 summary $OUT/ab.txt | cut -c1-300
+# the cost of the HIP-event steps in bench.py's timed region (every 4th step by default)
+for TE in 4 1000 4 1000; do
+  timeout -k 10 200 python bench.py --no-cpu --no-c4 --e2e-steps 0 --timing-every $TE > $OUT/bench_te$TE.json 2> $OUT/bench_te$TE.err || { tail -20 $OUT/bench_te$TE.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open('$OUT/bench_te$TE.json')); print('timing-every $TE', d['ms_per_step'], d['value'])"
+done
