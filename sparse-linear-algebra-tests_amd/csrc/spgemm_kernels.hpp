@@ -73,6 +73,9 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #define SLAT_SAT64_NARROW 1  // Sat64 rows under the u32 bound accumulate in u32 slots (variant builds: 0)
 #endif
 
+#ifndef SLAT_BM_MERGE
+#define SLAT_BM_MERGE 1  // bitmap passes: a group's same-word columns in one atomic (variant builds: 0)
+#endif
 constexpr int kPhaseSlots = 16;  // [0..12] phases, [15] rows
 
 // diagnostic builds: s_memtime phase accumulator (compiled away otherwise)
@@ -1312,12 +1315,39 @@ struct BitmapPass {
     uint32_t blk = 0;  // lane's mask of touched 64-word blocks (2048 columns each)
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &) {
         const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
+        if constexpr (SLAT_BM_MERGE) {
+            // a group is 4 consecutive entries of a sorted B row, so columns in one bitmap word are
+            // adjacent: their bits merge into the run's first atomic (a torus row's x-1, x, x+1
+            // usually share a word), fewer ds_or and fewer same-word conflicts between them
+            uint32_t w[4], m[4];
+            bool v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            uint32_t off;
-            if (win_off(cc[e], Z ? 0u : wlo, WIN, off)) {
-                atomicOr(&L0[(off >> 5) * STRIDE], 1u << (off & 31));
-                blk |= 1u << (off >> 11);
+            for (int e = 0; e < 4; ++e) {
+                uint32_t off = 0;
+                v[e] = win_off(cc[e], Z ? 0u : wlo, WIN, off);
+                w[e] = off >> 5;
+                m[e] = 1u << (off & 31);
+            }
+#pragma unroll
+            for (int e = 3; e > 0; --e) {
+                const bool same = v[e] && v[e - 1] && w[e] == w[e - 1];
+                m[e - 1] |= same ? m[e] : 0u;
+                v[e] = v[e] && !same;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (v[e]) {
+                    atomicOr(&L0[w[e] * STRIDE], m[e]);
+                    blk |= 1u << (w[e] >> 6);
+                }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                uint32_t off;
+                if (win_off(cc[e], Z ? 0u : wlo, WIN, off)) {
+                    atomicOr(&L0[(off >> 5) * STRIDE], 1u << (off & 31));
+                    blk |= 1u << (off >> 11);
+                }
             }
         }
     }
