@@ -74,7 +74,7 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #endif
 
 #ifndef SLAT_BM_MERGE
-#define SLAT_BM_MERGE 1  // bitmap passes: a group's same-word columns in one atomic (variant builds: 0)
+#define SLAT_BM_MERGE 0  // bitmap passes: a group's same-word columns in one atomic (variant builds: 1)
 #endif
 constexpr int kPhaseSlots = 16;  // [0..12] phases, [15] rows
 

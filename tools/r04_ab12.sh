@@ -1,5 +1,5 @@
 #!/bin/bash
-# bitmap passes with a group's same-word bits merged (k18) against one atomic per column (nomerge)
+# bitmap passes with a group's same-word bits merged (merge) against one atomic per column (k18)
 # and the previous tree (k17); C4's short-row
 # tiles of 64 rows (default) against 32 / 16 (SLAT_TILE_ROWS, now also for wide launches); parity first
 set -o pipefail
@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${1:-r04ab12}; mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest tests/test_spgemm_gpu.py -k "lane or golden or single_window or bitmap or torus" -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -n 1 $OUT/pytest.log
-timeout -k 10 700 python tools/ab.py --reps 2 --steps 100 --chain --c4 k17 nomerge k18 k18:SLAT_TILE_ROWS=32 k18:SLAT_TILE_ROWS=16 > $OUT/ab.txt 2>&1 || { tail -30 $OUT/ab.txt; exit 1; }
+timeout -k 10 900 python tools/ab.py --reps 2 --steps 100 --chain --c4 k17 merge k18 lr32 k18:SLAT_TILE_ROWS=32 k18:SLAT_TILE_ROWS=16 > $OUT/ab.txt 2>&1 || { tail -30 $OUT/ab.txt; exit 1; }
 grep -A5 summary $OUT/ab.txt | cut -c1-300
 # the cost of the HIP-event steps in bench.py's timed region (every 4th step by default)
 for TE in 4 1000 4 1000; do
