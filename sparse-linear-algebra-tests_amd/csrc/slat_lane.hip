@@ -43,6 +43,10 @@ constexpr uint32_t kLaneCap = 64;   // products per row (sort slots per lane)
 #endif
 constexpr uint32_t kLaneRows = SLAT_LANE_ROWS;  // rows per one-wave block (variant builds: 32)
 constexpr uint32_t kLaneSeg = 256;  // A entries / products per pass (four per lane)
+#ifndef SLAT_LANE_PG
+#define SLAT_LANE_PG 4
+#endif
+constexpr uint32_t kLanePG = SLAT_LANE_PG;  // product passes whose loads are issued together (variant builds: 1)
 
 template <typename S>
 __host__ __device__ constexpr size_t lane_lds() {
@@ -51,7 +55,7 @@ __host__ __device__ constexpr size_t lane_lds() {
     // row counts u32[64]
     // (+ u32 values: an output-value staging area u32[64 * rows], so the wave's outputs are stored
     // coalesced; the columns stage in the slot keys' area, free once the keys are in registers)
-    return (size_t)kLaneCap * kLaneRows * (4 + sizeof(S)) + kLaneSeg * (4 + sizeof(S) + 1 + 1 + 2) + kWave * 8 +
+    return (size_t)kLaneCap * kLaneRows * (4 + sizeof(S)) + kLaneSeg * (4 + sizeof(S) + 1 + 1 + 2 * kLanePG) + kWave * 8 +
            (sizeof(S) == 4 ? (size_t)kLaneCap * kLaneRows * 4 : 0);
 }
 
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
     uint8_t *erl = q + kLaneSeg * (4 + sizeof(S));
     uint8_t *amk = erl + kLaneSeg;
     uint16_t *pmk = (uint16_t *)(amk + kLaneSeg);
-    uint32_t *rbase = (uint32_t *)(pmk + kLaneSeg), *rcnt = rbase + kWave;
+    uint32_t *rbase = (uint32_t *)(pmk + kLaneSeg * kLanePG), *rcnt = rbase + kWave;
     S *stg = (S *)(rcnt + kWave);  // (u32 values) the outputs' value staging
     const uint32_t lane = (uint32_t)lane_id();
     const S *av = (const S *)p.a_val;
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
     }
     const uint32_t A0 = readlane_u32(A0j, 0), A1 = readlane_u32(A1j, (int)nt - 1);
     for (uint32_t w = lane; w < kLaneSeg / 4; w += kWave) ((uint32_t *)amk)[w] = 0;
-    for (uint32_t w = lane; w < kLaneSeg / 2; w += kWave) ((uint32_t *)pmk)[w] = 0;
+    for (uint32_t w = lane; w < kLaneSeg * kLanePG / 2; w += kWave) ((uint32_t *)pmk)[w] = 0;
     rcnt[lane] = 0;
     rbase[lane] = 0;
     wave_sync();
@@ -232,24 +236,26 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         });
         wave_sync();
         pc.mark(1);  // entries: rows, B row bounds, offsets
-        // the segment's products, 256 per pass: entry by markers, slot = t - the row's base
-        for (uint32_t p0 = 0; p0 < stot; p0 += kLaneSeg) {
+        // the segment's products, 256 per pass, kLanePG passes at a time (their loads in flight
+        // together): entry by markers, slot = t - the row's base
+        constexpr uint32_t kSpan = kLaneSeg * kLanePG, kQ = 4 * kLanePG;
+        for (uint32_t p0 = 0; p0 < stot; p0 += kSpan) {
             const uint32_t t0 = fcarry + p0;
             sfor<4>([&](auto Q) {
-                if (bl[Q] && off[Q] < t0 + kLaneSeg && off[Q] + bl[Q] > t0)
+                if (bl[Q] && off[Q] < t0 + kSpan && off[Q] + bl[Q] > t0)
                     pmk[max(off[Q], t0) - t0] = (uint16_t)(Q * kWave + lane + 1);
             });
             wave_sync();
-            uint32_t L[4], carry = 0;
-            sfor<4>([&](auto Q) {
+            uint32_t L[kQ], carry = 0;
+            sfor<kQ>([&](auto Q) {
                 const uint32_t m = pmk[Q * kWave + lane];
                 L[Q] = max(wave_incl_scan(m, 0u, mx), carry);
                 carry = readlane_u32(L[Q], kWave - 1);
             });
-            sfor<4>([&](auto Q) { pmk[Q * kWave + lane] = 0; });
-            uint32_t c[4], row[4], slot[4];
-            S v[4], a[4];
-            sfor<4>([&](auto Q) {
+            for (uint32_t w = lane; w < kSpan / 2; w += kWave) ((uint32_t *)pmk)[w] = 0;
+            uint32_t c[kQ], row[kQ], slot[kQ];
+            S v[kQ], a[kQ];
+            sfor<kQ>([&](auto Q) {
                 const uint32_t t = t0 + Q * kWave + lane;
                 c[Q] = kSent;
                 v[Q] = a[Q] = S(0);
@@ -264,7 +270,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
                     v[Q] = bv[bi];
                 }
             });
-            sfor<4>([&](auto Q) {
+            sfor<kQ>([&](auto Q) {
                 if (c[Q] != kSent && slot[Q] < kLaneCap) {
                     skey[slot[Q] * kLaneRows + row[Q]] = (c[Q] << 6) | slot[Q];
                     sval[slot[Q] * kLaneRows + row[Q]] = Sem::prod(a[Q], v[Q]);
