@@ -286,9 +286,10 @@ def main():
     ap.add_argument("--c4-steps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--e2e-steps", type=int, default=10, help="host-resident calls timed per mode (0: skip)")
-    ap.add_argument("--timing-every", type=int, default=4,
+    ap.add_argument("--timing-every", type=int, default=10,
                     help="record the per-kernel HIP events (roofline) on every k-th timed step; the event "
-                         "records cost host time, so the other steps run without them")
+                         "records and their read-back cost host time (every 4th step: +2 %% ms/step, "
+                         "profiles/r04_ab12.txt), so the other steps run without them")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -793,7 +793,14 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             const char *e = slat_ab_knob("SLAT_TILE_ROWS");
             return e ? (uint32_t)std::min(64, std::max(8, std::atoi(e))) : 0u;
         }();
-        if (asym.wide && kTileRows) a.tile_rows = asym.tile_rows = kTileRows;
+        if (asym.wide) {
+            // tiles of fewer rows when 64-row tiles would leave short-row waves idle: one rank's
+            // eighth of C4 (125 000 rows) took 0.49 ms in 64-row tiles (1953 tiles for ~5 000 waves),
+            // 0.32 / 0.30 / 0.29 in 32 / 16 / 8; the whole C4 (1 M rows) 1.27 ms in 64-row tiles,
+            // 1.29 / 1.30 / 1.35 in smaller ones (profiles/r04_ab12.txt): about 32 tiles per CU
+            const uint64_t t = n / ((uint64_t)ctx->cu_count * 32);
+            a.tile_rows = asym.tile_rows = kTileRows ? kTileRows : (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, t));
+        }
         if (!asym.wide) {
             a.sym_cap = asym.sym_cap = kHashT / 2;  // every counted row fits numeric's table
             // tiles of fewer rows when 64-row tiles would leave most resident waves idle (27 000 rows:

@@ -272,6 +272,9 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
 #ifndef SLAT_FOLD_PREFETCH
 #define SLAT_FOLD_PREFETCH 1
 #endif
+#ifndef SLAT_FOLD_DEPTH
+#define SLAT_FOLD_DEPTH 4  // fold-order walk: entries whose B loads are in flight together (variant builds: 1)
+#endif
 constexpr uint32_t kFlatHuge = 1u << 24;  // parts at least this long: walked by the whole wave alone
 // ORDERED (f64 in the reference's fold order): the wave walks every entry of the row itself, in A
 // order (each wave owns its own slice of the chunk's columns), and fn(c, a, b, valid) is called by the
@@ -618,39 +621,67 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                 load_part(kA, bs_now, be_now);
             }
             unsigned long long m = __ballot(bs_now != be_now);
-            uint32_t cn = 0;
-            S vn = S(0), an = S(0);
-            I sn = 0, en = 0;
-            auto fetch = [&](int t) {
-                sn = (I)readlane_u64((uint64_t)bs_now, t);
-                en = (I)readlane_u64((uint64_t)be_now, t);
-                an = readlane_val(a_now, t);
-                if (sn + (I)lane < en) {
-                    cn = p.b_col[sn + (I)lane];
-                    vn = bv[sn + (I)lane];
-                }
+            // the group's entries with a non-empty part, in A order, kFD at a time: the next kFD
+            // entries' B loads are issued before this kFD's products are added (adds stay in entry
+            // order; only the loads move ahead)
+            constexpr int kFD = SLAT_FOLD_DEPTH;
+            struct Ent {
+                uint32_t c[kFD];
+                S v[kFD], a[kFD];
+                I s[kFD], e[kFD];
             };
-            if (m) fetch((int)__builtin_ctzll(m));
-            while (m) {
-                const uint32_t c = cn;
-                const S v = vn, at = an;
-                const I s = sn, e = en;
-                m &= m - 1;
-                if (m) fetch((int)__builtin_ctzll(m));
-                if (s + (I)lane < e) {
-                    const uint32_t o = c - c0;
-                    acc[o] = __dadd_rn(acc[o], __dmul_rn(at, v));
-                    atomicOr(&bits[o >> 5], 1u << (o & 31));
-                }
-                wave_sync();  // this entry's adds land before the next entry's (same columns)
-                for (I j0 = s + (I)kWave; j0 < e; j0 += (I)kWave) {  // a part longer than a wave
-                    const I j = j0 + (I)lane;
-                    if (j < e) {
-                        const uint32_t o = p.b_col[j] - c0;
-                        acc[o] = __dadd_rn(acc[o], __dmul_rn(at, bv[j]));
-                        atomicOr(&bits[o >> 5], 1u << (o & 31));
+            auto fetch = [&](Ent &q) {
+                sfor<kFD>([&](auto U) {
+                    q.s[U] = q.e[U] = 0;
+                    q.a[U] = q.v[U] = S(0);
+                    q.c[U] = 0;
+                    if (m) {
+                        const int t = (int)__builtin_ctzll(m);
+                        m &= m - 1;
+                        q.s[U] = (I)readlane_u64((uint64_t)bs_now, t);
+                        q.e[U] = (I)readlane_u64((uint64_t)be_now, t);
+                        q.a[U] = readlane_val(a_now, t);
+                        if (q.s[U] + (I)lane < q.e[U]) {
+                            q.c[U] = p.b_col[q.s[U] + (I)lane];
+                            q.v[U] = bv[q.s[U] + (I)lane];
+                        }
                     }
-                    wave_sync();
+                });
+            };
+            auto apply = [&](const Ent &q) {
+                sfor<kFD>([&](auto U) {
+                    const I s = q.s[U], e = q.e[U];
+                    if (s != e) {  // wave-uniform
+                        if (s + (I)lane < e) {
+                            const uint32_t o = q.c[U] - c0;
+                            acc[o] = __dadd_rn(acc[o], __dmul_rn(q.a[U], q.v[U]));
+                            atomicOr(&bits[o >> 5], 1u << (o & 31));
+                        }
+                        wave_sync();  // this entry's adds land before the next entry's (same columns)
+                        for (I j0 = s + (I)kWave; j0 < e; j0 += (I)kWave) {  // a part longer than a wave
+                            const I j = j0 + (I)lane;
+                            if (j < e) {
+                                const uint32_t o = p.b_col[j] - c0;
+                                acc[o] = __dadd_rn(acc[o], __dmul_rn(q.a[U], bv[j]));
+                                atomicOr(&bits[o >> 5], 1u << (o & 31));
+                            }
+                            wave_sync();
+                        }
+                    }
+                });
+            };
+            if (m) {
+                Ent qa, qb;
+                fetch(qa);
+                for (;;) {
+                    const bool mb = m != 0;
+                    if (mb) fetch(qb);
+                    apply(qa);
+                    if (!mb) break;
+                    const bool ma = m != 0;
+                    if (ma) fetch(qa);
+                    apply(qb);
+                    if (!ma) break;
                 }
             }
         }
