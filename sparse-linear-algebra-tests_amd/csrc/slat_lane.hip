@@ -308,7 +308,21 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         // (the max row first, its result waited for: it is in place once a later block sees this
         // block's status, so the last block reads the final max after its look-back)
         if (lane == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | rmax));
-        const unsigned long long excl = lookback_prefix_wave(status, blockIdx.x, epoch, agg);
+        // the aggregate published first; u32 rows then stage their outputs in LDS at the wave-local
+        // offset while the earlier blocks finish, and only the coalesced store waits for the offset
+        lookback_publish(status, blockIdx.x, epoch, agg);
+        uint32_t zeros = 0;
+        if constexpr (sizeof(S) == 4) {
+            const uint32_t o0 = incl - nz;
+            if (nz)
+                zeros = lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
+                    skey[o0 + j] = col;
+                    stg[o0 + j] = val;
+                });
+            wave_sync();
+        }
+        pc.mark(7);  // (u32) the outputs staged
+        const unsigned long long excl = lookback_walk(status, blockIdx.x, epoch, agg);
         if (lane == 0) {
             if (blockIdx.x == gridDim.x - 1) {
                 const unsigned long long mw = __hip_atomic_load(maxw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -326,17 +340,9 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
             p.c_rp[r + 1] = base + nz;
             if (r == 0) p.c_rp[0] = 0;
         }
-        uint32_t zeros = 0;
         if constexpr (sizeof(S) == 4) {
-            // the wave's rows are contiguous in C: outputs staged in LDS at their wave offset, then
-            // stored coalesced (the scattered per-lane stores cost one instruction per output)
-            const uint32_t o0 = incl - nz;
-            if (nz)
-                zeros = lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
-                    skey[o0 + j] = col;
-                    stg[o0 + j] = val;
-                });
-            wave_sync();
+            // the wave's rows are contiguous in C: the staged outputs stored coalesced (scattered
+            // per-lane stores cost one instruction per output)
             uint32_t *oc = p.c_col + excl;
             S *ov = (S *)p.c_val + excl;
             for (uint32_t u = lane; u < agg; u += kWave) {
@@ -356,7 +362,7 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
         // (as after k_numeric)
         if (lane < nt) p.counts[r] = nz - zeros;
         add_zero_rows(&p.host_out[2], wave_sum_u32(zeros ? 1u : 0u), true);
-        pc.mark(7);  // row_ptr, the emit
+        pc.mark(8);  // row_ptr, the emit
     };
     if (wmax <= 16)
         body(std::integral_constant<int, 16>{});

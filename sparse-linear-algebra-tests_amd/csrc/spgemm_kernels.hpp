@@ -405,6 +405,9 @@ __device__ __forceinline__ uint32_t sat32(S v) {
 // of kOrdAhead consecutive entries are loaded before any of them is visited, so the visits (in A
 // order: the left fold of linalg/src/csr.rs:325-337) do not wait on one load chain per entry.
 constexpr int kOrdAhead = 8;
+#ifndef SLAT_ORD_DB
+#define SLAT_ORD_DB 1  // the next kOrdAhead entries' loads under this kOrdAhead's visits (variant builds: 0)
+#endif
 template <typename I, typename S, typename F>
 __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&visit) {
     const int lane = lane_id();
@@ -423,31 +426,56 @@ __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&
             }
         }
         const int cnt = (int)min<uint64_t>((uint64_t)kWave, (uint64_t)(a1 - base));
-        for (int t0 = 0; t0 < cnt; t0 += kOrdAhead) {
-            uint32_t pc[kOrdAhead];
-            S pv[kOrdAhead];
+        struct Ahead {
+            uint32_t c[kOrdAhead];
+            S v[kOrdAhead];
+        };
+        auto fetch = [&](int t0, Ahead &q) {
             sfor<kOrdAhead>([&](auto G) {
-                pc[G] = kSent;
-                pv[G] = S(0);
+                q.c[G] = kSent;
+                q.v[G] = S(0);
                 const int t = t0 + G;
                 if (t < cnt) {
                     const I s = (I)readlane_u64((uint64_t)bs, t), e = (I)readlane_u64((uint64_t)be, t);
                     const I jdx = s + (I)lane;
                     if (jdx < e) {
-                        pc[G] = p.b_col[jdx];
-                        pv[G] = bv_[jdx];
+                        q.c[G] = p.b_col[jdx];
+                        q.v[G] = bv_[jdx];
                     }
                 }
             });
+        };
+        auto visit_all = [&](int t0, const Ahead &q) {
             sfor<kOrdAhead>([&](auto G) {
                 const int t = t0 + G;
                 if (t < cnt) {
                     const I s = (I)readlane_u64((uint64_t)bs, t), e = (I)readlane_u64((uint64_t)be, t);
                     const S a = readlane_val(av, t);
-                    if (pc[G] != kSent) visit(pc[G], a, pv[G]);
+                    if (q.c[G] != kSent) visit(q.c[G], a, q.v[G]);
                     for (I jdx = s + (I)kWave + (I)lane; jdx < e; jdx += (I)kWave) visit(p.b_col[jdx], a, bv_[jdx]);
                 }
             });
+        };
+        if constexpr (SLAT_ORD_DB) {
+            // double-buffered: the next kOrdAhead entries' loads are issued before this kOrdAhead
+            // are visited (visits stay in A order)
+            Ahead qa, qb;
+            if (cnt > 0) fetch(0, qa);
+            for (int t0 = 0; t0 < cnt; t0 += 2 * kOrdAhead) {
+                const bool hb = t0 + kOrdAhead < cnt;
+                if (hb) fetch(t0 + kOrdAhead, qb);
+                visit_all(t0, qa);
+                if (!hb) break;
+                const bool ha = t0 + 2 * kOrdAhead < cnt;
+                if (ha) fetch(t0 + 2 * kOrdAhead, qa);
+                visit_all(t0 + kOrdAhead, qb);
+            }
+        } else {
+            for (int t0 = 0; t0 < cnt; t0 += kOrdAhead) {
+                Ahead q;
+                fetch(t0, q);
+                visit_all(t0, q);
+            }
         }
     }
 }
@@ -2763,19 +2791,24 @@ __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long l
 // dependent load per predecessor. Many small tiles arriving together (k_lane: ~400 one-wave blocks)
 // made the lane-0 walk a chain of hundreds of loads. Called by every lane of the wave; returns the
 // tile's exclusive prefix in every lane.
-__device__ __forceinline__ unsigned long long lookback_prefix_wave(unsigned long long *status, uint64_t tile,
-                                                                   uint32_t epoch, unsigned long long agg) {
+// (split in two: lookback_publish stores the tile's aggregate (tile 0: its inclusive prefix), and
+// lookback_walk reads the predecessors, so a caller can do work that does not need the offset in between)
+__device__ __forceinline__ void lookback_publish(unsigned long long *status, uint64_t tile, uint32_t epoch,
+                                                 unsigned long long agg) {
+    const unsigned long long tag = (unsigned long long)epoch << 42;
+    if (lane_id() == 0)
+        __hip_atomic_store(&status[tile], tag | (tile == 0 ? kStInc : kStAgg) | agg, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long lookback_walk(unsigned long long *status, uint64_t tile, uint32_t epoch,
+                                                            unsigned long long agg) {
     auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     auto st = [](unsigned long long *x, unsigned long long v) {
         __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     const int lane = lane_id();
     const unsigned long long tag = (unsigned long long)epoch << 42;
-    if (tile == 0) {
-        if (lane == 0) st(&status[0], tag | kStInc | agg);
-        return 0;
-    }
-    if (lane == 0) st(&status[tile], tag | kStAgg | agg);
+    if (tile == 0) return 0;
     unsigned long long excl = 0;
     for (int64_t j0 = (int64_t)tile - 1;; j0 -= kWave) {
         const int64_t j = j0 - lane;
@@ -2799,6 +2832,11 @@ __device__ __forceinline__ unsigned long long lookback_prefix_wave(unsigned long
     }
     if (lane == 0) st(&status[tile], tag | kStInc | (excl + agg));
     return excl;
+}
+__device__ __forceinline__ unsigned long long lookback_prefix_wave(unsigned long long *status, uint64_t tile,
+                                                                   uint32_t epoch, unsigned long long agg) {
+    lookback_publish(status, tile, epoch, agg);
+    return lookback_walk(status, tile, epoch, agg);
 }
 
 
