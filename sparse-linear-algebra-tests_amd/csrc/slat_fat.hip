@@ -273,7 +273,7 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
 #define SLAT_FOLD_PREFETCH 1
 #endif
 #ifndef SLAT_FOLD_DEPTH
-#define SLAT_FOLD_DEPTH 4  // fold-order walk: entries whose B loads are in flight together (variant builds: 1)
+#define SLAT_FOLD_DEPTH 16  // fold-order walk: entries whose B loads are in flight together (variant builds: 1, 4, 8)
 #endif
 constexpr uint32_t kFlatHuge = 1u << 24;  // parts at least this long: walked by the whole wave alone
 // ORDERED (f64 in the reference's fold order): the wave walks every entry of the row itself, in A
