@@ -76,6 +76,12 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_BM_MERGE
 #define SLAT_BM_MERGE 0  // bitmap passes: a group's same-word columns in one atomic (variant builds: 1)
 #endif
+#ifndef SLAT_ROW_PREFETCH
+#define SLAT_ROW_PREFETCH 0  // k_numeric (single-window): the next row's bounds loaded ahead (variant builds: 1)
+#endif
+#ifndef SLAT_SYM_PREFETCH
+#define SLAT_SYM_PREFETCH 0  // k_symbolic (single-window): the next row's bounds loaded ahead (variant builds: 1)
+#endif
 constexpr int kPhaseSlots = 16;  // [0..12] phases, [15] rows
 
 // diagnostic builds: s_memtime phase accumulator (compiled away otherwise)
@@ -1506,10 +1512,11 @@ __host__ __device__ constexpr bool sym_short_row(uint64_t len, uint32_t b_maxrow
 constexpr uint64_t kNoRow = ~0ull;
 template <typename I, bool ELL, int MODE>
 __device__ __forceinline__ uint64_t sym_row(const Args &p, uint64_t row, bool listed, uint32_t *L0,
-                                            unsigned long long &flops) {
+                                            unsigned long long &flops, bool have = false, uint64_t pa0 = 0,
+                                            uint64_t pa1 = 0) {
     const int lane = lane_id();
     const uint32_t WIN = p.ww * 32;
-    const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
+    const I a0 = have ? (I)pa0 : (I)p.a_rp[row], a1 = have ? (I)pa1 : (I)p.a_rp[row + 1];
     if constexpr (MODE != 0) {
         if (!listed && sym_short_row((uint64_t)(a1 - a0), p.b_maxrow) != (MODE == 1)) return kNoRow;  // the other launch's row
     }
@@ -1637,11 +1644,25 @@ void k_symbolic(Args p) {
     const bool dyn = MODE != 0 && p.tq != nullptr;  // launch-uniform
     const TicketQueue tq(p.tq, nit, stride);
     unsigned long long pend = 0;
+    // (SLAT_SYM_PREFETCH, single-window passes) the next row's bounds loaded by lanes 0-1 ahead
+    constexpr bool kPre = SLAT_SYM_PREFETCH && MODE == 0;
+    uint64_t pre = 0;
+    auto prefetch = [&](uint64_t r) {
+        if constexpr (kPre)
+            if (r < nit && lane < 2) pre = p.a_rp[r + lane];
+    };
+    prefetch((uint64_t)blockIdx.x * kWpb + wv);
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
         if (dyn) pend = tq.issue();
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
+        uint64_t pa0 = 0, pa1 = 0;
+        if constexpr (kPre) {
+            pa0 = readlane_u64(pre, 0);
+            pa1 = readlane_u64(pre, 1);
+            prefetch(it + stride);
+        }
         if (fat_row(p, row)) continue;  // the fat-row kernels' row
-        const uint64_t cnt = sym_row<I, ELL, MODE>(p, row, listed, L0, flops);
+        const uint64_t cnt = sym_row<I, ELL, MODE>(p, row, listed, L0, flops, kPre, pa0, pa1);
         if (cnt == kNoRow) continue;
         if (lane == 0) p.counts[row] = cnt;
         mx = max(mx, cnt);
@@ -1732,12 +1753,44 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
     const bool dyn = MODE != 0 && p.tq != nullptr;  // launch-uniform (single-window passes: a fixed stride)
     const TicketQueue tq(p.tq, nit, stride);
     unsigned long long pend = 0;
+    // (SLAT_ROW_PREFETCH, single-window passes) the next row's bounds, C offsets and stored block mask
+    // loaded by lanes 0-4 while this row runs: one dependent latency less per row
+    constexpr bool kPre = SLAT_ROW_PREFETCH && MODE == 0;
+    uint64_t pre = 0;
+    auto prefetch = [&](uint64_t r) {
+        if constexpr (kPre) {
+            if (r < nit) {
+                if (lane < 2)
+                    pre = p.a_rp[r + lane];
+                else if (lane < 4)
+                    pre = p.c_rp[r + lane - 2];
+                else if (lane == 4 && p.smask)
+                    pre = p.smask[r];
+            }
+        }
+    };
+    prefetch(first);
     for (uint64_t it = first; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
         if (dyn) pend = tq.issue();
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
+        I a0, a1;
+        uint64_t out_begin, out_end;
+        uint32_t pmask = 0;
+        if constexpr (kPre) {
+            a0 = (I)readlane_u64(pre, 0);
+            a1 = (I)readlane_u64(pre, 1);
+            out_begin = readlane_u64(pre, 2);
+            out_end = readlane_u64(pre, 3);
+            pmask = (uint32_t)readlane_u64(pre, 4);
+            prefetch(it + stride);
+        }
         if (fat_row(p, row)) continue;  // the fat-row kernels' row
-        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
-        const uint64_t out_begin = p.c_rp[row], out_end = p.c_rp[row + 1];
+        if constexpr (!kPre) {
+            a0 = (I)p.a_rp[row];
+            a1 = (I)p.a_rp[row + 1];
+            out_begin = p.c_rp[row];
+            out_end = p.c_rp[row + 1];
+        }
         uint64_t out_pos = out_begin;
         uint32_t zeros = 0;
         ph[kPhaseSlots - 1] += 1;
@@ -1846,7 +1899,7 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
                     //     at a time, ranked from registers and written whole ({bits, rank} per word),
                     //     so untouched blocks may hold stale words (no valid column reads them) and
                     //     nothing is cleared afterwards
-                    bmask = __builtin_amdgcn_readfirstlane(p.smask[row]);
+                    bmask = kPre ? pmask : __builtin_amdgcn_readfirstlane(p.smask[row]);
                     const uint32_t *src = p.sbm + row * ((uint64_t)p.nblk * kWave) + lane;
                     uint32_t m = bmask;
                     while (m) {
