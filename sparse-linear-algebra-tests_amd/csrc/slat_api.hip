@@ -76,7 +76,7 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         delete ctx;
         return SLAT_EOOM;
     }
-    if (hipMalloc((void **)&ctx->d_words, 64) != hipSuccess || hipMemset(ctx->d_words, 0, 64) != hipSuccess ||
+    if (hipMalloc((void **)&ctx->d_words, 128) != hipSuccess || hipMemset(ctx->d_words, 0, 128) != hipSuccess ||
         hipHostMalloc((void **)&ctx->h_out, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&ctx->h_out_dev, ctx->h_out, 0) != hipSuccess) {
         (void)hipHostFree(ctx->h_shards);
@@ -420,9 +420,10 @@ static uint32_t build_ell_blocks(const slat_csr_view *B, uint32_t wq) {
 
 template <typename S>
 static hipError_t launch_build_ell(hipStream_t s, const slat_csr_view *B, uint32_t wq, uint32_t *ecol, void *eval,
-                                   uint8_t *eng, unsigned long long *part) {
+                                   uint8_t *eng, unsigned long long *part, const unsigned long long *rng = nullptr,
+                                   uint32_t epoch = 0) {
     hipLaunchKernelGGL(k_build_ell<S>, dim3(build_ell_blocks(B, wq)), dim3(kBlock), 0, s, B->row_ptr, B->col_idx,
-                       (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng, part);
+                       (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng, part, rng, epoch);
     return hipGetLastError();
 }
 
@@ -901,15 +902,30 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // the ELL image (or B's value summary) first: it runs while the host allocates C and queues
     // the rest, instead of after the host's setup with the GPU idle
     if (ell) {
+        // a row block of A (the strong-scaling ranks' calls): only the B rows its columns reference go
+        // into the image (their range from k_col_range, read on the device: no round trip), so the
+        // build shrinks with the block instead of costing the whole B on every rank
+        const unsigned long long *rng = nullptr;
+        uint32_t repoch = 0;
+        static const bool kNoEllRange = slat_ab_knob("SLAT_NO_ELL_RANGE") != nullptr;  // A/B knob
+        if (n < A->n_rows && !kNoEllRange) {
+            rng = ctx->d_words + 8;
+            repoch = ++ctx->epoch;
+            const unsigned g = (unsigned)std::max<uint64_t>(
+                1, std::min<uint64_t>((a_nnz_block + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4));
+            hipLaunchKernelGGL(k_col_range, dim3(g), dim3(kBlock), 0, s, a.a_rp, n, A->col_idx, ctx->d_words + 8, repoch);
+            SLAT_HIP(ctx, hipGetLastError());
+        }
         hipError_t be;
         if (dt == SLAT_U32)
             be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
-                                            (unsigned long long *)(ws + o_part));
+                                            (unsigned long long *)(ws + o_part), rng, repoch);
         else if (dt == SLAT_SAT64)
             be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
-                                                      (unsigned long long *)(ws + o_part));
+                                                      (unsigned long long *)(ws + o_part), rng, repoch);
         else
-            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
+            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr,
+                                          rng, repoch);
         SLAT_HIP(ctx, be);
     } else if (a.b_vmax && B->nnz) {
         const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);

@@ -42,7 +42,8 @@ struct slat_ctx {
     unsigned long long done_seq = 0;         // last sequence number queued to [7]
     unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word,
                                              // [4] check flags, [5] work tickets (zeroed by each launch's last taker),
-                                             // [6] blocks done of the call's last kernel (zeroed by its last block)
+                                             // [6] blocks done of the call's last kernel (zeroed by its last block),
+                                             // [8] / [9] a row block's column range (k_col_range, epoch-tagged)
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
     unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)

@@ -493,15 +493,30 @@ __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&
 // B entries, the B row pointers drop out of the dependent load chain (a_col -> ELL row), and
 // rows are 16-byte aligned. Built per call into the context workspace (a few microseconds).
 // ------------------------------------------------------------------------------------------------
+// rng (row-block calls, optional): only B rows [lo, hi] are built, the column range of A's row block
+// from k_col_range ([0] (epoch << 32) | ~lo, [1] (epoch << 32) | hi; another epoch: no entries), so
+// the image's build time and bytes shrink with the block (no other B row is ever read)
 template <typename S>
 __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const uint32_t *col, const S *val,
                                                        uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng,
-                                                       unsigned long long *part) {
+                                                       unsigned long long *part, const unsigned long long *rng = nullptr,
+                                                       uint32_t epoch = 0) {
     // one thread per (row k, group t): 4 columns and 4 values, written as whole groups
     // 32-bit group index: the host keeps n < 2^24 and wq <= 8 for the ELL copy
     uint32_t mx = 0, mn = 0xFFFFFFFFu;
-    const uint32_t total = n * wq;
-    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < total; g += gridDim.x * kBlock) {
+    uint32_t g0 = 0, total = n * wq;
+    if (rng) {
+        const unsigned long long l = rng[0], h = rng[1];
+        g0 = total = 0;
+        if ((uint32_t)(l >> 32) == epoch && (uint32_t)(h >> 32) == epoch) {
+            const uint32_t lo = ~(uint32_t)l, hi = min((uint32_t)h, n - 1);
+            if (lo <= hi) {
+                g0 = lo * wq;
+                total = (hi + 1) * wq;
+            }
+        }
+    }
+    for (uint32_t g = g0 + blockIdx.x * kBlock + threadIdx.x; g < total; g += gridDim.x * kBlock) {
         const uint32_t k = g / wq;
         const uint32_t t = g - k * wq;
         const uint64_t s0 = rp[k], len = rp[k + 1] - s0;
@@ -546,6 +561,37 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
                 mn = min(mn, bn[w]);
             }
             part[blockIdx.x] = ((unsigned long long)~mn << 32) | mx;
+        }
+    }
+}
+
+// the column range of A's row block [rp[0], rp[n]): rng[0] = (epoch << 32) | ~min, rng[1] = (epoch << 32) |
+// max, one atomic pair per block (k_build_ell's row range for row-block calls)
+static __global__ __launch_bounds__(kBlock) void k_col_range(const uint64_t *rp, uint64_t n, const uint32_t *col,
+                                                      unsigned long long *rng, uint32_t epoch) {
+    const uint64_t j0 = rp[0], j1 = rp[n];
+    uint32_t mx = 0, mn = 0xFFFFFFFFu;
+    for (uint64_t j = j0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < j1; j += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t c = col[j];
+        mx = max(mx, c);
+        mn = min(mn, c);
+    }
+    __shared__ uint32_t bm[kBlock / kWave], bn[kBlock / kWave];
+    mx = wave_max_u32(mx);
+    mn = wave_min_u32(mn);
+    if (lane_id() == 0) {
+        bm[threadIdx.x / kWave] = mx;
+        bn[threadIdx.x / kWave] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) {
+            mx = max(mx, bm[w]);
+            mn = min(mn, bn[w]);
+        }
+        if (mn <= mx) {
+            atomicMax(&rng[0], ((unsigned long long)epoch << 32) | ~mn);
+            atomicMax(&rng[1], ((unsigned long long)epoch << 32) | mx);
         }
     }
 }

@@ -312,6 +312,30 @@ def test_rowblock_partition_concatenates_to_full(ctx):
     np.testing.assert_array_equal(np.concatenate(vals), full.values)
 
 
+@pytest.mark.parametrize("dtype", [slat.U32, slat.SAT64, slat.F64])
+def test_rowblock_ell_built_over_referenced_rows(ctx, dtype):
+    # row blocks of A^3 * A take B's ELL image built only over the B rows the block's columns reach
+    # (k_col_range -> k_build_ell's row range): one-row blocks, the first and last rows (the range at
+    # either end of B), a middle stretch, and blocks in both orders on one context (stale ranges of an
+    # earlier call must not leak into the next)
+    a = O.torus_thinned(16, 3.0, O.Rng())
+    a3 = O.matmul_seq(O.matmul_seq(a, a), a)
+    full = O.matmul_seq(a3, a)
+    rp, col, val = full.arrays()
+    P, B = to_dev(a3, dtype), to_dev(a, dtype)
+    n = a.n
+    blocks = [(0, 1), (n - 1, n), (0, 300), (n - 300, n), (n // 2, n // 2 + 700), (n // 3, n // 3 + 1), (5, n - 5)]
+    for lo, hi in blocks + blocks[::-1]:
+        h = P.matmul_rowblock(lo, hi, B, slat.FLAG_NO_TINY).host()  # (the pipeline: blocks <= 2048 rows would run one kernel)
+        s0, s1 = int(rp[lo]), int(rp[hi])
+        np.testing.assert_array_equal(h.row_ptr, rp[lo:hi + 1] - rp[lo], err_msg=f"[{lo},{hi}) row_ptr")
+        np.testing.assert_array_equal(h.col_idx, col[s0:s1], err_msg=f"[{lo},{hi}) col_idx")
+        if val.dtype == np.float64:
+            np.testing.assert_array_equal(h.values.view(np.uint64), val[s0:s1].view(np.uint64))
+        else:
+            np.testing.assert_array_equal(h.values, val[s0:s1], err_msg=f"[{lo},{hi}) values")
+
+
 def test_empty_and_ragged(ctx):
     for n in (1, 2, 65, 1000):
         z = slat.CsrMatrix.new(n)
