@@ -902,13 +902,15 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // the ELL image (or B's value summary) first: it runs while the host allocates C and queues
     // the rest, instead of after the host's setup with the GPU idle
     if (ell) {
-        // a row block of A (the strong-scaling ranks' calls): only the B rows its columns reference go
-        // into the image (their range from k_col_range, read on the device: no round trip), so the
-        // build shrinks with the block instead of costing the whole B on every rank
+        // (A/B knob SLAT_ELL_RANGE) a row block of A: only the B rows its columns reference go into
+        // the image (their range from k_col_range, read on the device: no round trip). Measured slower
+        // on one rank's eighth of C4 (0.30 -> 0.30-0.33 ms, profiles/r04_ab16.txt): the range kernel's
+        // same-address atomics cost more than the smaller build saves, and a torus block's wrapped
+        // neighbours make the edge blocks' range all of B anyway
         const unsigned long long *rng = nullptr;
         uint32_t repoch = 0;
-        static const bool kNoEllRange = slat_ab_knob("SLAT_NO_ELL_RANGE") != nullptr;  // A/B knob
-        if (n < A->n_rows && !kNoEllRange) {
+        static const bool kEllRange = slat_ab_knob("SLAT_ELL_RANGE") != nullptr;
+        if (n < A->n_rows && kEllRange) {
             rng = ctx->d_words + 8;
             repoch = ++ctx->epoch;
             const unsigned g = (unsigned)std::max<uint64_t>(

@@ -80,7 +80,7 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #define SLAT_ROW_PREFETCH 0  // k_numeric (single-window): the next row's bounds loaded ahead (variant builds: 1)
 #endif
 #ifndef SLAT_SYM_PREFETCH
-#define SLAT_SYM_PREFETCH 0  // k_symbolic (single-window): the next row's bounds loaded ahead (variant builds: 1)
+#define SLAT_SYM_PREFETCH 1  // k_symbolic (single-window): the next row's bounds loaded ahead (variant builds: 0)
 #endif
 constexpr int kPhaseSlots = 16;  // [0..12] phases, [15] rows
 
