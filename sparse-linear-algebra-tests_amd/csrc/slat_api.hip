@@ -704,9 +704,14 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // max row(B) is <= 4 caps; a row past the cap sets the mapped overflow word and the call reruns
     // through the pipeline. Column ids < 2^26 (the sort keys carry a 6-bit slot)
     static const bool kNoLane = slat_ab_knob("SLAT_NO_LANE") != nullptr;
-    const bool lane = !kNoLane && !tiny && idx32 && wait_mode() == 0 && !ablate && ncols <= (1ull << 26) &&
-                      !(flags & (SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) && g_progress.load(std::memory_order_relaxed) == 0 &&
-                      A->max_row_nnz && (unsigned __int128)A->max_row_nnz * maxrow_b <= 4 * slat_lane_cap();
+    bool lane = !kNoLane && !tiny && idx32 && wait_mode() == 0 && !ablate && ncols <= (1ull << 26) &&
+                !(flags & (SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) && g_progress.load(std::memory_order_relaxed) == 0 &&
+                A->max_row_nnz && (unsigned __int128)A->max_row_nnz * maxrow_b <= 4 * slat_lane_cap();
+    // (a bound above one cap may overflow: a pair that did is sent to the pipeline from then on. The
+    // 30^3 sweep's e/n-4 cell overflowed on every call and paid both paths, 95 -> 149 us)
+    if (lane && (unsigned __int128)A->max_row_nnz * maxrow_b > slat_lane_cap())
+        for (const auto &m : ctx->lane_miss)
+            if (m.a_col == A->col_idx && m.b_col == B->col_idx && m.a_nnz == A->nnz && m.b_nnz == B->nnz) lane = false;
     static const bool kNoEll = slat_ab_knob("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
@@ -1047,6 +1052,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         hc.mark(6);
         SLAT_HIPC(wait_stream(ctx, s, a.seq));
         if (ctx->h_out[3]) {
+            ctx->lane_miss[ctx->lane_miss_next++ % 8] = {A->col_idx, B->col_idx, A->nnz, B->nnz};
             // a row of more than slat_lane_cap() products: the call through the pipeline
             (void)failc(SLAT_OK);
             return slat_spgemm_rowblock(ctx, A, row_begin, row_end, B, C, flags | SLAT_FLAG_NO_TINY);

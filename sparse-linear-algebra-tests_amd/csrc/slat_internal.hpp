@@ -46,6 +46,14 @@ struct slat_ctx {
                                              // [8] / [9] a row block's column range (k_col_range, epoch-tagged)
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
+    // operand pairs whose lane-kernel attempt overflowed (a row past slat_lane_cap() products): the
+    // next call on the same pair goes to the pipeline directly instead of running both. Keyed by the
+    // arrays' addresses and sizes; a stale hit after a free / alloc only costs that call the pipeline
+    struct LaneMiss {
+        const void *a_col, *b_col;
+        uint64_t a_nnz, b_nnz;
+    } lane_miss[8] = {};
+    uint32_t lane_miss_next = 0;
     unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
     uint64_t status_cap = 0;                 // tiles d_status holds
     unsigned long long ticket_base = 0;      // tiles handed out so far (the ticket is monotonic)

@@ -556,3 +556,7 @@ def test_lane_rows(ctx, dtype, case):
         assert ctx.stats()["mode"] & 8, "the lane kernel did not run"
     assert_same(got, want, f"lane rows {case}")
     assert_same(da._spgemm(db, slat.FLAG_NO_TINY), want, f"pipeline {case}")
+    if case == "overflow":
+        # the pair is remembered: the next call goes to the pipeline without the lane attempt
+        assert_same(da._spgemm(db), want, "overflow, second call")
+        assert not ctx.stats()["mode"] & 8, "the remembered pair ran the lane kernel again"
