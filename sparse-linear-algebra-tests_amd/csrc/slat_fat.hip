@@ -272,6 +272,9 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
 #ifndef SLAT_FOLD_PREFETCH
 #define SLAT_FOLD_PREFETCH 1
 #endif
+#ifndef SLAT_FR_UNI
+#define SLAT_FR_UNI 1  // the flattened walk skips B-value loads for a pattern B (variant builds: 0)
+#endif
 #ifndef SLAT_FOLD_DEPTH
 #define SLAT_FOLD_DEPTH 16  // fold-order walk: entries whose B loads are in flight together (variant builds: 1, 4, 8)
 #endif
@@ -490,7 +493,7 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
             // a pattern B (every value equal, k_bvmax's epoch-tagged max and ~min): no value loads
             bool uni = false;
             S v0 = S(0);
-            if constexpr (Sem::kNarrowable)
+            if constexpr (Sem::kNarrowable && SLAT_FR_UNI)
                 if (p.b_vmax) {
                     const unsigned long long vx = ((volatile unsigned long long *)p.b_vmax)[kVMaxWord];
                     const unsigned long long vi = ((volatile unsigned long long *)p.b_vmax)[kVMinInvWord];
