@@ -273,7 +273,7 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
 #define SLAT_FOLD_PREFETCH 1
 #endif
 #ifndef SLAT_FR_UNI
-#define SLAT_FR_UNI 1  // the flattened walk skips B-value loads for a pattern B (variant builds: 0)
+#define SLAT_FR_UNI 0  // the flattened walk skips B-value loads for a pattern B (variant builds: 1): measured slower, RG 4.17 -> 6.04 ms (profiles/r04_ab19.txt)
 #endif
 #ifndef SLAT_FOLD_DEPTH
 #define SLAT_FOLD_DEPTH 16  // fold-order walk: entries whose B loads are in flight together (variant builds: 1, 4, 8)
