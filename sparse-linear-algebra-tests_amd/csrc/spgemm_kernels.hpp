@@ -76,6 +76,9 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_BM_MERGE
 #define SLAT_BM_MERGE 0  // bitmap passes: a group's same-word columns in one atomic (variant builds: 1)
 #endif
+#ifndef SLAT_NUM_UNI
+#define SLAT_NUM_UNI 1  // k_numeric / k_numeric_short: no B-value loads for a pattern B (variant builds: 0)
+#endif
 #ifndef SLAT_ROW_PREFETCH
 #define SLAT_ROW_PREFETCH 0  // k_numeric (single-window): the next row's bounds loaded ahead (variant builds: 1)
 #endif
@@ -1769,7 +1772,8 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
                 bvmax = (uint32_t)v;
                 // (a wider value type clamps to u32 in the summary: all-equal clamped values are
                 // not a pattern unless below the clamp)
-                buni = (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax && (sizeof(S) == 4 || bvmax != 0xFFFFFFFFu);
+                buni = SLAT_NUM_UNI && (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax &&
+                       (sizeof(S) == 4 || bvmax != 0xFFFFFFFFu);
             }
         }
     const S bv0 = (S)bvmax;
@@ -2639,7 +2643,8 @@ __device__ __forceinline__ void numeric_short_body(Args p) {
                 bvmax = (uint32_t)v;
                 // (a wider value type clamps to u32 in the summary: all-equal clamped values are
                 // not a pattern unless below the clamp)
-                buni = (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax && (sizeof(S) == 4 || bvmax != 0xFFFFFFFFu);
+                buni = SLAT_NUM_UNI && (uint32_t)(vi >> 32) == p.epoch && ~(uint32_t)vi == bvmax &&
+                       (sizeof(S) == 4 || bvmax != 0xFFFFFFFFu);
             }
         }
     const S bv0 = (S)bvmax;
