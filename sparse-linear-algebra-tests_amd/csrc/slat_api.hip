@@ -77,6 +77,7 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         return SLAT_EOOM;
     }
     if (hipMalloc((void **)&ctx->d_words, 128) != hipSuccess || hipMemset(ctx->d_words, 0, 128) != hipSuccess ||
+        hipMalloc((void **)&ctx->d_done, kDoneBytes) != hipSuccess || hipMemset(ctx->d_done, 0, kDoneBytes) != hipSuccess ||
         hipHostMalloc((void **)&ctx->h_out, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&ctx->h_out_dev, ctx->h_out, 0) != hipSuccess) {
         (void)hipHostFree(ctx->h_shards);
@@ -96,9 +97,11 @@ slat_status slat_ctx_destroy(slat_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
+    slat_hostio_destroy(ctx);
     dev_release_all(ctx);
     if (ctx->h_shards) (void)hipHostFree(ctx->h_shards);
     if (ctx->d_words) (void)hipFree(ctx->d_words);
+    if (ctx->d_done) (void)hipFree(ctx->d_done);
     if (ctx->h_out) (void)hipHostFree(ctx->h_out);
     for (auto &e : ctx->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->own_stream);
@@ -254,6 +257,8 @@ void slat_dev_free(slat_ctx *ctx, void *p, hipStream_t s) {
     if (it == ctx->live.end()) return;  // not ours (or freed already)
     slat_ctx::Block b = it->second;
     ctx->live.erase(it);
+    for (auto &m : ctx->lane_miss)
+        if (m.a_rp == p || m.a_col == p || m.b_rp == p || m.b_col == p) m = {};
     b.s = s;
     cache_put(ctx, b);
     if (ctx->cache_bytes > kCacheMax) {
@@ -339,15 +344,25 @@ extern "C" slat_status slat_csr_create(slat_ctx *ctx, const slat_csr_view *src, 
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
     std::memset(out, 0, sizeof *out);
     const size_t vs = vsize(src->dtype);
-    const hipMemcpyKind kind = src->residency == SLAT_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
     SLAT_HIP(ctx, alloc_joint(ctx, out, src->n_rows, src->nnz, vs, ctx->stream));
-    if (src->n_rows)
-        SLAT_HIP(ctx, hipMemcpyAsync(out->row_ptr, src->row_ptr, (src->n_rows + 1) * 8, kind, ctx->stream));
-    else
-        SLAT_HIP(ctx, hipMemsetAsync(out->row_ptr, 0, 8, ctx->stream));
-    if (src->nnz) {
-        SLAT_HIP(ctx, hipMemcpyAsync(out->col_idx, src->col_idx, src->nnz * 4, kind, ctx->stream));
-        SLAT_HIP(ctx, hipMemcpyAsync(out->values, src->values, src->nnz * vs, kind, ctx->stream));
+    if (!src->n_rows) SLAT_HIP(ctx, hipMemsetAsync(out->row_ptr, 0, 8, ctx->stream));
+    if (src->residency == SLAT_HOST) {
+        // host arrays (the drop-in's Vecs): the staging ring for pageable memory (slat_hostio.hip)
+        const slat_hostseg segs[3] = {{(void *)src->row_ptr, out->row_ptr, src->n_rows ? (src->n_rows + 1) * 8 : 0},
+                                      {(void *)src->col_idx, out->col_idx, src->nnz * 4},
+                                      {(void *)src->values, out->values, src->nnz * vs}};
+        if ((st = slat_copy_h2d(ctx, segs, 3))) {
+            slat_csr_free(ctx, out);
+            return st;
+        }
+    } else {
+        const hipMemcpyKind kind = hipMemcpyDeviceToDevice;
+        if (src->n_rows)
+            SLAT_HIP(ctx, hipMemcpyAsync(out->row_ptr, src->row_ptr, (src->n_rows + 1) * 8, kind, ctx->stream));
+        if (src->nnz) {
+            SLAT_HIP(ctx, hipMemcpyAsync(out->col_idx, src->col_idx, src->nnz * 4, kind, ctx->stream));
+            SLAT_HIP(ctx, hipMemcpyAsync(out->values, src->values, src->nnz * vs, kind, ctx->stream));
+        }
     }
     out->n_rows = src->n_rows;
     out->n_cols = src->n_cols;
@@ -376,7 +391,14 @@ extern "C" slat_status slat_csr_to_host(slat_ctx *ctx, const slat_csr_view *src,
     slat_status st = slat_check_view(ctx, src, "src");
     if (st) return st;
     SLAT_HIP(ctx, hipSetDevice(ctx->device));
-    const hipMemcpyKind kind = src->residency == SLAT_HOST ? hipMemcpyHostToHost : hipMemcpyDeviceToHost;
+    if (src->residency != SLAT_HOST) {
+        // device -> the caller's host arrays: the staging ring for pageable memory (slat_hostio.hip)
+        const slat_hostseg segs[3] = {{row_ptr, (void *)src->row_ptr, row_ptr ? (src->n_rows + 1) * 8 : 0},
+                                      {col, (void *)src->col_idx, col ? src->nnz * 4 : 0},
+                                      {vals, (void *)src->values, vals ? src->nnz * vsize(src->dtype) : 0}};
+        return slat_copy_d2h(ctx, segs, 3);
+    }
+    const hipMemcpyKind kind = hipMemcpyHostToHost;
     if (row_ptr) SLAT_HIP(ctx, hipMemcpyAsync(row_ptr, src->row_ptr, (src->n_rows + 1) * 8, kind, ctx->stream));
     if (src->nnz && col) SLAT_HIP(ctx, hipMemcpyAsync(col, src->col_idx, src->nnz * 4, kind, ctx->stream));
     if (src->nnz && vals) SLAT_HIP(ctx, hipMemcpyAsync(vals, src->values, src->nnz * vsize(src->dtype), kind, ctx->stream));
@@ -420,10 +442,9 @@ static uint32_t build_ell_blocks(const slat_csr_view *B, uint32_t wq) {
 
 template <typename S>
 static hipError_t launch_build_ell(hipStream_t s, const slat_csr_view *B, uint32_t wq, uint32_t *ecol, void *eval,
-                                   uint8_t *eng, unsigned long long *part, const unsigned long long *rng = nullptr,
-                                   uint32_t epoch = 0) {
+                                   uint8_t *eng, unsigned long long *part) {
     hipLaunchKernelGGL(k_build_ell<S>, dim3(build_ell_blocks(B, wq)), dim3(kBlock), 0, s, B->row_ptr, B->col_idx,
-                       (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng, part, rng, epoch);
+                       (const S *)B->values, (uint32_t)B->n_rows, wq, ecol, (S *)eval, eng, part);
     return hipGetLastError();
 }
 
@@ -639,13 +660,30 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     }
     uint64_t maxrow_b = B->max_row_nnz;
     if (maxrow_b == 0 && (st = slat_csr_max_row_nnz(ctx, B, &maxrow_b))) return st;
-    // A entries of the row block (C's capacity bound): the whole A's nnz, then rows x A's max row
-    // when known (no sync); a block whose bound is still large reads its two row_ptr words (one
-    // small round trip, against a call that takes milliseconds at that size)
+    // C's capacity by the exact bound nnz(A block) x max row(B) (no mid-call sync) unless it exceeds
+    // the budget: free device memory / 4 (re-read when this context's pool grew or shrank, else every
+    // 1024 calls: the query costs tens of microseconds of host time) and at most kBoundBytes (a loose
+    // bound, power-law B: nnz(A) x a hub row, would make every call allocate and release tens of GB,
+    // which costs far more than the exact path's one sync). Decided before the kernel choice: the
+    // one-kernel paths (tiny, lane) need the bound-sized C, so an exact call takes the pipeline with
+    // its ELL image, stored bitmaps and hash batches
+    if (ctx->mem_changed || ctx->free_age++ % 1024 == 0) {
+        size_t total_b = 0;
+        (void)hipMemGetInfo(&ctx->free_b, &total_b);
+        ctx->mem_changed = false;
+    }
+    static const uint64_t kBoundBytes = [] {
+        const char *e = slat_ab_knob("SLAT_BOUND_MAX_BYTES");
+        return e ? std::strtoull(e, nullptr, 10) : (4ull << 30);
+    }();
+    const unsigned __int128 budget = std::min<unsigned __int128>(ctx->free_b / 4, kBoundBytes);
+    // A entries of the row block: the whole A's nnz, then rows x A's max row when known (no sync);
+    // only a block whose bound is still over the budget reads its two row_ptr words (one round trip,
+    // which cost a row-block call ~15 us of its ~300: one rank's eighth of C4)
     uint64_t a_nnz_block = A->nnz;
     if (n < A->n_rows) {
         if (A->max_row_nnz) a_nnz_block = std::min<uint64_t>(a_nnz_block, n * A->max_row_nnz);
-        if ((unsigned __int128)a_nnz_block * maxrow_b * (4 + vs) > (256ull << 20)) {
+        if ((unsigned __int128)a_nnz_block * maxrow_b * (4 + vs) > budget) {
             SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards, A->row_ptr + row_begin, 8, hipMemcpyDeviceToHost, ctx->stream));
             SLAT_HIP(ctx, hipMemcpyAsync(ctx->h_shards + 1, A->row_ptr + row_end, 8, hipMemcpyDeviceToHost, ctx->stream));
             SLAT_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -654,6 +692,10 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             a_nnz_block = ctx->h_shards[1] - ctx->h_shards[0];
         }
     }
+    unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
+    const unsigned __int128 dense = (unsigned __int128)n * ncols;
+    if (bound128 > dense) bound128 = dense;
+    bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
 
     Args a = {};
     a.a_rp = A->row_ptr + row_begin;
@@ -694,7 +736,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // finishes in microseconds, no fat rows, and no per-pass timing or stats (those report the
     // regular pipeline's passes)
     static const bool kNoTiny = slat_ab_knob("SLAT_NO_TINY") != nullptr;
-    const bool tiny = !kNoTiny && !asym.wide && ncols <= 8192 && n <= 2048 && idx32 && wait_mode() == 0 && !ablate &&
+    const bool tiny = !kNoTiny && !exact && !asym.wide && ncols <= 8192 && n <= 2048 && idx32 && wait_mode() == 0 && !ablate &&
                       !(flags & (SLAT_FLAG_TIMING | SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) &&
                       g_progress.load(std::memory_order_relaxed) == 0 &&
                       (unsigned __int128)a_nnz_block * maxrow_b <= (1u << 18) &&
@@ -702,50 +744,30 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // rows of at most slat_lane_cap() products: the whole call in one kernel, a row per lane
     // (slat_lane.hip: C1, the 30^3 chain's A * A, 88 -> ~25 us). Tried when the bound max row(A) x
     // max row(B) is <= 4 caps; a row past the cap sets the mapped overflow word and the call reruns
-    // through the pipeline. Column ids < 2^26 (the sort keys carry a 6-bit slot)
+    // through the pipeline. Column ids < 2^26 - 1: the sort key (column << 6) | slot of column 2^26 - 1
+    // at slot 63 would equal the padding key kSent
     static const bool kNoLane = slat_ab_knob("SLAT_NO_LANE") != nullptr;
-    bool lane = !kNoLane && !tiny && idx32 && wait_mode() == 0 && !ablate && ncols <= (1ull << 26) &&
+    bool lane = !kNoLane && !exact && !tiny && idx32 && wait_mode() == 0 && !ablate && ncols < (1ull << 26) &&
                 !(flags & (SLAT_FLAG_STATS | SLAT_FLAG_NO_TINY)) && g_progress.load(std::memory_order_relaxed) == 0 &&
                 A->max_row_nnz && (unsigned __int128)A->max_row_nnz * maxrow_b <= 4 * slat_lane_cap();
     // (a bound above one cap may overflow: a pair that did is sent to the pipeline from then on. The
     // 30^3 sweep's e/n-4 cell overflowed on every call and paid both paths, 95 -> 149 us)
     if (lane && (unsigned __int128)A->max_row_nnz * maxrow_b > slat_lane_cap())
         for (const auto &m : ctx->lane_miss)
-            if (m.a_col == A->col_idx && m.b_col == B->col_idx && m.a_nnz == A->nnz && m.b_nnz == B->nnz) lane = false;
+            if (m.a_rp == A->row_ptr && m.a_col == A->col_idx && m.b_rp == B->row_ptr && m.b_col == B->col_idx &&
+                m.a_nnz == A->nnz && m.b_nnz == B->nnz && m.a_rows == A->n_rows && m.row_begin == row_begin &&
+                m.row_end == row_end)
+                lane = false;
     static const bool kNoEll = slat_ab_knob("SLAT_NO_ELL") != nullptr;
     const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
                      B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
                      !kNoEll && !tiny && !lane;  // 24-bit row index, 31-bit byte offsets in the kernels
     // stored bitmaps (single-window launches): symbolic keeps each row's touched bitmap blocks for
     // numeric, n * ww words at most (only touched blocks are written), capped against free memory
-    // free device memory: re-read when this context's pool grew or shrank, else every 1024 calls
-    // (the query costs tens of microseconds of host time)
-    if (ctx->mem_changed || ctx->free_age++ % 1024 == 0) {
-        size_t total_b = 0;
-        (void)hipMemGetInfo(&ctx->free_b, &total_b);
-        ctx->mem_changed = false;
-    }
     const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
     static const bool kNoSbm = slat_ab_knob("SLAT_NO_SBM") != nullptr;
     const bool sbm = !a.wide && sbm_words * 4 <= std::max<uint64_t>(256ull << 20, ctx->free_b / 16) && !kNoSbm && !tiny &&
                      !lane;
-    // a workgroup per row (slat_group.hip): single-window launches with B in ELL form. Symbolic for
-    // every value type; numeric for the semirings that add with atomics (f64 in the reference's fold
-    // order keeps the ordered wave-per-row walk), reading symbolic's stored bitmaps
-    // (SLAT_GROUP=1: the workgroup-per-row kernels for the long rows instead of the wave-per-row ones;
-    // measured slower on the 30^3 chain)
-    static const bool kNoGroup = slat_ab_knob("SLAT_GROUP") == nullptr;
-    // threads per row of the group kernels (A/B knobs SLAT_GRP_SYM_T / SLAT_GRP_NUM_T: 128 or 256)
-    static const int kGrpSymT = [] {
-        const char *e = slat_ab_knob("SLAT_GRP_SYM_T");
-        return e && std::atoi(e) == 256 ? 256 : 128;
-    }();
-    static const int kGrpNumT = [] {
-        const char *e = slat_ab_knob("SLAT_GRP_NUM_T");
-        return e && std::atoi(e) == 128 ? 128 : 256;
-    }();
-    const bool gsym = !a.wide && ell && !tiny && !kNoGroup && !ablate;
-    const bool gnum = gsym && sbm && (dt != SLAT_F64 || f64any);
     static const bool kNoHash = slat_ab_knob("SLAT_NO_HASH") != nullptr;
     // single-window launches (the 30^3 chain, configs C1 / C2 / C3) batch their short rows the same way
     // (MAGNUS's small-row category) when the workgroup kernels take the rest: rows of <= 256 products
@@ -875,7 +897,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
-    const size_t o_bmax = o_fat + fat_b,  // per-block max counts (the group kernels' grid: <= 8 blocks per CU)
+    const size_t o_bmax = o_fat + fat_b,  // per-block max counts (the symbolic grid)
         bmax_b = up256((size_t)std::max<uint64_t>(sym_grid.x, (uint64_t)ctx->cu_count * 8) * 4);
     if ((st = slat_ensure_ws(ctx, o_bmax + bmax_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
@@ -907,32 +929,15 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // the ELL image (or B's value summary) first: it runs while the host allocates C and queues
     // the rest, instead of after the host's setup with the GPU idle
     if (ell) {
-        // (A/B knob SLAT_ELL_RANGE) a row block of A: only the B rows its columns reference go into
-        // the image (their range from k_col_range, read on the device: no round trip). Measured slower
-        // on one rank's eighth of C4 (0.30 -> 0.30-0.33 ms, profiles/r04_ab16.txt): the range kernel's
-        // same-address atomics cost more than the smaller build saves, and a torus block's wrapped
-        // neighbours make the edge blocks' range all of B anyway
-        const unsigned long long *rng = nullptr;
-        uint32_t repoch = 0;
-        static const bool kEllRange = slat_ab_knob("SLAT_ELL_RANGE") != nullptr;
-        if (n < A->n_rows && kEllRange) {
-            rng = ctx->d_words + 8;
-            repoch = ++ctx->epoch;
-            const unsigned g = (unsigned)std::max<uint64_t>(
-                1, std::min<uint64_t>((a_nnz_block + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4));
-            hipLaunchKernelGGL(k_col_range, dim3(g), dim3(kBlock), 0, s, a.a_rp, n, A->col_idx, ctx->d_words + 8, repoch);
-            SLAT_HIP(ctx, hipGetLastError());
-        }
         hipError_t be;
         if (dt == SLAT_U32)
             be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
-                                            (unsigned long long *)(ws + o_part), rng, repoch);
+                                            (unsigned long long *)(ws + o_part));
         else if (dt == SLAT_SAT64)
             be = launch_build_ell<unsigned long long>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
-                                                      (unsigned long long *)(ws + o_part), rng, repoch);
+                                                      (unsigned long long *)(ws + o_part));
         else
-            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr,
-                                          rng, repoch);
+            be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
         SLAT_HIP(ctx, be);
     } else if (a.b_vmax && B->nnz) {
         const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
@@ -969,19 +974,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         }
     }
     hc.mark(3);
-    // capacity by exact bound (no mid-call sync) unless it exceeds the budget
-    unsigned __int128 bound128 = (unsigned __int128)a_nnz_block * maxrow_b;
-    const unsigned __int128 dense = (unsigned __int128)n * ncols;
-    if (bound128 > dense) bound128 = dense;
-    // free device memory: refreshed every 32 calls above (the query costs host time on every call)
-    // and at most kBoundBytes: a loose bound (power-law B: nnz(A) x a hub row) would make every call
-    // allocate and release tens of GB, which costs far more than the exact path's one sync
-    static const uint64_t kBoundBytes = [] {
-        const char *e = slat_ab_knob("SLAT_BOUND_MAX_BYTES");
-        return e ? std::strtoull(e, nullptr, 10) : (4ull << 30);
-    }();
-    const unsigned __int128 budget = std::min<unsigned __int128>(ctx->free_b / 4, kBoundBytes);
-    bool exact = (flags & SLAT_FLAG_EXACT_ALLOC) || bound128 * (4 + vs) > budget;
+    // capacity by the bound computed above (exact: the exact-size path)
     // C's arrays in three pieces: row_ptr, then col_idx and values sized by the bound; after the
     // call both are trimmed to nnz(C) and their tails go back to the context's cache
     SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&C->row_ptr, (n + 1) * 8, s));
@@ -1025,7 +1018,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         a.c_col = C->col_idx;
         a.c_val = C->values;
         a.seq = ++ctx->done_seq;
-        a.done = ctx->d_words + 6;
+        a.done = ctx->d_done;
         const uint64_t g = row_blocks;
         if ((st = ensure_status(ctx, g, s))) return failc(st);
         const uint32_t epoch = slat_next_scan_epoch(ctx, s);
@@ -1039,7 +1032,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         a.c_col = C->col_idx;
         a.c_val = C->values;
         a.seq = ++ctx->done_seq;
-        a.done = ctx->d_words + 6;
+        a.done = ctx->d_done;
         const uint64_t g = (n + slat_lane_rows() - 1) / slat_lane_rows();
         if ((st = ensure_status(ctx, g, s))) return failc(st);
         const uint32_t epoch = slat_next_scan_epoch(ctx, s);
@@ -1052,7 +1045,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         hc.mark(6);
         SLAT_HIPC(wait_stream(ctx, s, a.seq));
         if (ctx->h_out[3]) {
-            ctx->lane_miss[ctx->lane_miss_next++ % 8] = {A->col_idx, B->col_idx, A->nnz, B->nnz};
+            ctx->lane_miss[ctx->lane_miss_next++ % 8] = {A->row_ptr, A->col_idx, B->row_ptr, B->col_idx, A->nnz,
+                                                         B->nnz,     A->n_rows,   row_begin, row_end};
             // a row of more than slat_lane_cap() products: the call through the pipeline
             (void)failc(SLAT_OK);
             return slat_spgemm_rowblock(ctx, A, row_begin, row_end, B, C, flags | SLAT_FLAG_NO_TINY);
@@ -1116,12 +1110,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         h2.tq = (kDyn & 2u) && asym.wide ? tq : nullptr;  // (single-window rows: a fixed stride)
         if (all_short) {
             // (no listed rows)
-        } else if (asym.wide || !gsym) {
+        } else {
             SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
-        } else {  // the listed rows by the workgroup kernel (stored bitmaps for numeric)
-            const size_t glds = (size_t)asym.ww * 4;
-            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(kGrpSymT, sem, false, idx32, glds, asym.ww);
-            SLAT_HIPC(slat_launch_group_symbolic(kGrpSymT, idx32, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb))), glds, s, h2));
         }
         a.list = all_short ? nullptr : (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
         a.list_cnt = all_short ? nullptr : lc + 16;
@@ -1133,17 +1123,8 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     } else {
         // single-window launch without fat rows: symbolic leaves per-block max row counts for the
         // scan's last tile (<= 16 per scan thread)
-        if (gsym) {
-            const size_t glds = (size_t)asym.ww * 4;
-            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(kGrpSymT, sem, false, idx32, glds, asym.ww);
-            const dim3 gg((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb)));
-            if (!fat && gg.x <= 16u * kScanThreads && gg.x * 4 <= bmax_b) asym.bmax = (uint32_t *)(ws + o_bmax);
-            SLAT_HIPC(slat_launch_group_symbolic(kGrpSymT, idx32, gg, glds, s, asym));
-            sym_blocks = gg.x;
-        } else {
-            if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
-            SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
-        }
+        if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
+        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
     }
     hc.mark(5);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
@@ -1169,18 +1150,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     a.c_col = C->col_idx;
     a.c_val = C->values;
     const int win_mode = hash ? 2 : 0;  // numeric instance of the window rows
-    auto launch_num = [&](const Args &x) {
-        if (gnum && !a.wide) {
-            // a workgroup per row: ~12 KB of rank slots (2048 narrow outputs in one chunk)
-            Args g = x;
-            g.area = 12288;
-            const size_t glds = slat_group_numeric_lds(g.ww, g.area);
-            const uint64_t gb = (uint64_t)ctx->cu_count * slat_group_blocks_per_cu(kGrpNumT, sem, true, idx32, glds, g.ww);
-            const dim3 gg((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(n, gb)));
-            return slat_launch_group_numeric(kGrpNumT, sem, idx32, gg, glds, s, g);
-        }
-        return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x);
-    };
+    auto launch_num = [&](const Args &x) { return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x); };
     if (ablate & ~7u) {
         // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
         // the real numeric pass below overwrites everything it wrote
@@ -1201,14 +1171,14 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         h1.tq = (kDyn & 2u) && hash_mode != 3 ? tq : nullptr;
         if (all_short && fused) {
             a.seq = h1.seq = ++ctx->done_seq;
-            h1.done = ctx->d_words + 6;
+            h1.done = ctx->d_done;
         }
         SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
     }
     a.tq = (kDyn & 2u) && hash && a.wide ? tq : nullptr;  // (single-window rows: a fixed stride)
     if (fused && !all_short) {
         a.seq = ++ctx->done_seq;
-        a.done = ctx->d_words + 6;
+        a.done = ctx->d_done;
     }
     if (!all_short) SLAT_HIPC(launch_num(a));
     if (wsplit) slat_dev_free(ctx, wsplit, s);  // stream-ordered: reused only by later work

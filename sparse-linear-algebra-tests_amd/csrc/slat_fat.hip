@@ -266,27 +266,13 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
 #ifndef SLAT_FR_FLAT
 #define SLAT_FR_FLAT 1
 #endif
-#ifndef SLAT_FR_FLAT_ORD
-#define SLAT_FR_FLAT_ORD 0
-#endif
-#ifndef SLAT_FOLD_PREFETCH
-#define SLAT_FOLD_PREFETCH 1
-#endif
-#ifndef SLAT_FR_UNI
-#define SLAT_FR_UNI 0  // the flattened walk skips B-value loads for a pattern B (variant builds: 1): measured slower, RG 4.17 -> 6.04 ms (profiles/r04_ab19.txt)
-#endif
 #ifndef SLAT_FOLD_DEPTH
 #define SLAT_FOLD_DEPTH 16  // fold-order walk: entries whose B loads are in flight together (variant builds: 1, 4, 8)
 #endif
 constexpr uint32_t kFlatHuge = 1u << 24;  // parts at least this long: walked by the whole wave alone
-// ORDERED (f64 in the reference's fold order): the wave walks every entry of the row itself, in A
-// order (each wave owns its own slice of the chunk's columns), and fn(c, a, b, valid) is called by the
-// whole wave once per slot of 64 products, slots in position order, so it can keep each column's
-// products in entry order; otherwise fn(c, a, b) per product.
-// uni: every B value equals v0 (a pattern B, from k_bvmax's summary): no B-value loads
-template <typename S, bool VALS, typename I, bool ORDERED = false, typename Part, typename F>
-__device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, F &&fn, uint8_t *wl, bool uni = false,
-                                        S v0 = S(0)) {
+// fn(c, a, b) per product.
+template <typename S, bool VALS, typename I, typename Part, typename F>
+__device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, F &&fn, uint8_t *wl) {
     const int lane = lane_id();
     const int wv = threadIdx.x / kWave;
     I *eb = (I *)wl;
@@ -296,11 +282,9 @@ __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, 
     const S *bv = (const S *)p.b_val;
     const auto plus = [](uint32_t x, uint32_t y) { return x + y; };
     const auto mx = [](uint32_t x, uint32_t y) { return max(x, y); };
-    // wave w's entries: w, w + 8, w + 16, ... (a row of 100 entries keeps all 8 waves busy);
-    // ORDERED: all of them, 64 at a time
-    constexpr I kStep = ORDERED ? (I)kWave : (I)kFB;
-    for (I base = a0 + (ORDERED ? (I)0 : (I)wv); base < a1; base += kStep) {
-        const I i = base + (I)lane * (ORDERED ? (I)1 : (I)kFW);
+    // wave w's entries: w, w + 8, w + 16, ... (a row of 100 entries keeps all 8 waves busy)
+    for (I base = a0 + (I)wv; base < a1; base += (I)kFB) {
+        const I i = base + (I)lane * (I)kFW;
         I bs = 0;
         uint32_t len = 0;
         S a = S(0);
@@ -309,9 +293,7 @@ __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, 
             if constexpr (VALS) a = av[i];
             if (k < p.b_nrows) part(k, bs, len);
         }
-        // a part of 2^24 or more entries on its own (the flat offsets stay below 2^30; an ordered
-        // slice part is at most the slice's width)
-        if constexpr (!ORDERED)
+        // a part of 2^24 or more entries on its own (the flat offsets stay below 2^30)
         for (unsigned long long m = __ballot(len >= kFlatHuge); m; m &= m - 1) {
             const int l0 = (int)__builtin_ctzll(m);
             const I s0 = (I)readlane_u64((uint64_t)bs, l0);
@@ -347,17 +329,14 @@ __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, 
                     const I bi = eb[l] + (I)j;
                     c[E] = p.b_col[bi];
                     if constexpr (VALS) {
-                        v[E] = uni ? v0 : bv[bi];
+                        v[E] = bv[bi];
                         aa[E] = ea[l];
                     }
                 }
             });
-            if constexpr (ORDERED)
-                sfor<4>([&](auto E) { fn(c[E], aa[E], v[E], c[E] != kSent); });
-            else
-                sfor<4>([&](auto E) {
-                    if (c[E] != kSent) fn(c[E], aa[E], v[E]);
-                });
+            sfor<4>([&](auto E) {
+                if (c[E] != kSent) fn(c[E], aa[E], v[E]);
+            });
             wave_sync();  // the markers clear before the next pass writes them
         }
     }
@@ -490,17 +469,6 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
     const uint32_t g0 = c0 >> f.gsh, g1 = min(f.nch1 - 1, (c1 + (1u << f.gsh) - 1) >> f.gsh);
     if constexpr (!Sem::kOrdered && SLAT_FR_FLAT) {
         if (f.split) {  // the chunk's part of each B row from the split table: no filtering
-            // a pattern B (every value equal, k_bvmax's epoch-tagged max and ~min): no value loads
-            bool uni = false;
-            S v0 = S(0);
-            if constexpr (Sem::kNarrowable && SLAT_FR_UNI)
-                if (p.b_vmax) {
-                    const unsigned long long vx = ((volatile unsigned long long *)p.b_vmax)[kVMaxWord];
-                    const unsigned long long vi = ((volatile unsigned long long *)p.b_vmax)[kVMinInvWord];
-                    uni = (uint32_t)(vx >> 32) == p.epoch && (uint32_t)(vi >> 32) == p.epoch &&
-                          ~(uint32_t)vi == (uint32_t)vx && (sizeof(S) == 4 || (uint32_t)vx != 0xFFFFFFFFu);
-                    v0 = (S)(uint32_t)vx;
-                }
             fr_flat<S, true, I>(
                 p, a0, a1,
                 [&](uint32_t k, I &bs, uint32_t &len) {
@@ -514,7 +482,7 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                     Sem::acc(acc, o, Sem::prod(a, b));
                     atomicOr(&bits[o >> 5], 1u << (o & 31));
                 },
-                wl, uni, v0);
+                wl);
             return;
         }
     }
@@ -532,49 +500,8 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
         const int lane = lane_id(), wv = threadIdx.x / kWave;
         const uint32_t g = g0 + (uint32_t)wv;
         if ((c0 + ((uint32_t)wv << f.gsh)) >= c1) return;
-        if constexpr (SLAT_FR_FLAT_ORD) {
-            // (variant builds -DSLAT_FR_FLAT_ORD=1) the wave's slice flattened over the row's entries
-            // (every lane on a product, whatever the parts' lengths), slots of 64 products in A order.
-            // Within a slot the lanes are in position order, so lanes on one column apply their
-            // products lowest lane first: the column's same-column lanes by one ballot per offset bit,
-            // then rounds by rank (one round unless two entries of the slot meet on a column).
-            // Measured slower than the per-entry walk below (C5 2^16 fold 12.0 -> 13.0 ms, 2^18
-            // 96.0 -> 100.5, profiles/r04_ab6.txt): a wave slice gets ~0.4 products per A entry, so
-            // the per-64-entry loads and scans outweigh the idle lanes they save
-            const uint32_t sw = 1u << f.gsh, s0 = c0 + ((uint32_t)wv << f.gsh);
-            const uint64_t lt = (1ull << lane) - 1;
-            fr_flat<S, true, I, true>(
-                p, a0, a1,
-                [&](uint32_t k, I &bs, uint32_t &len) {
-                    const uint32_t *sp = f.split + (uint64_t)k * f.nch1 + g;
-                    const uint32_t q0 = sp[0];
-                    bs = (I)p.b_rp[k] + (I)q0;
-                    len = sp[1] - q0;
-                },
-                [&](uint32_t c, S a, S b, bool valid) {
-                    const uint32_t ol = valid ? c - s0 : 0u;  // offset in the slice
-                    unsigned long long same = __ballot(valid);
-                    for (uint32_t bit = 1; bit < sw; bit <<= 1) {
-                        const unsigned long long bb = __ballot(valid && (ol & bit));
-                        same &= (ol & bit) ? bb : ~bb;
-                    }
-                    const uint32_t rank = valid ? (uint32_t)__popcll(same & lt) : 0u;
-                    const uint32_t rmax = wave_max_u32(rank);
-                    const uint32_t o = ol + (s0 - c0);
-                    for (uint32_t r = 0; r <= rmax; ++r) {
-                        if (valid && rank == r) {
-                            acc[o] = __dadd_rn(acc[o], __dmul_rn(a, b));
-                            atomicOr(&bits[o >> 5], 1u << (o & 31));
-                        }
-                        wave_sync();
-                    }
-                },
-                wl);
-            return;
-        }
         // 64 entries at a time, the next groups' loads in flight under this group's products: the
-        // entries two groups ahead, the B parts (bounds + split) one group ahead (variant builds
-        // -DSLAT_FOLD_PREFETCH=0: each group's loads when it starts)
+        // entries two groups ahead, the B parts (bounds + split) one group ahead
         auto load_k = [&](I base, uint32_t &k, S &a) {
             const I i = base + (I)lane;
             k = kSent;
@@ -605,24 +532,13 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
             I bsB, beB;
             uint32_t kC;
             S aC;
-            if constexpr (SLAT_FOLD_PREFETCH) {
-                load_part(kB, bsB, beB);
-                load_k(base + (I)(2 * kWave), kC, aC);
-            } else {
-                bsB = beB = 0;
-                kC = kSent;
-                aC = S(0);
-            }
+            load_part(kB, bsB, beB);
+            load_k(base + (I)(2 * kWave), kC, aC);
             bsA = bsB;
             beA = beB;
             aA = aB;
             kB = kC;
             aB = aC;
-            if constexpr (!SLAT_FOLD_PREFETCH) {  // this group's loads now (the round-3 walk)
-                load_k(base, kA, aA);
-                a_now = aA;
-                load_part(kA, bs_now, be_now);
-            }
             unsigned long long m = __ballot(bs_now != be_now);
             // the group's entries with a non-empty part, in A order, kFD at a time: the next kFD
             // entries' B loads are issued before this kFD's products are added (adds stay in entry

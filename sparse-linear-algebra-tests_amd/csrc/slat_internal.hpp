@@ -25,6 +25,8 @@ inline const char *slat_ab_knob(const char *name) {
 #endif
 }
 
+struct slat_hostio;  // the page-locked staging ring and its copy threads (slat_hostio.hip)
+
 struct slat_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -42,16 +44,17 @@ struct slat_ctx {
     unsigned long long done_seq = 0;         // last sequence number queued to [7]
     unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word,
                                              // [4] check flags, [5] work tickets (zeroed by each launch's last taker),
-                                             // [6] blocks done of the call's last kernel (zeroed by its last block),
-                                             // [8] / [9] a row block's column range (k_col_range, epoch-tagged)
+                                             // [6] unused,
+    unsigned long long *d_done = nullptr;    // the call's last kernel's two-level done count (signal_done)
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
-    // operand pairs whose lane-kernel attempt overflowed (a row past slat_lane_cap() products): the
-    // next call on the same pair goes to the pipeline directly instead of running both. Keyed by the
-    // arrays' addresses and sizes; a stale hit after a free / alloc only costs that call the pipeline
+    // (A, B, row block) triples whose lane-kernel attempt overflowed (a row past slat_lane_cap()
+    // products): the next call on the same triple goes to the pipeline directly instead of running
+    // both. Keyed by both operands' arrays, sizes and the row range; an entry whose array the context
+    // frees is dropped (slat_dev_free), so a new matrix at a recycled address starts clean
     struct LaneMiss {
-        const void *a_col, *b_col;
-        uint64_t a_nnz, b_nnz;
+        const void *a_rp, *a_col, *b_rp, *b_col;
+        uint64_t a_nnz, b_nnz, a_rows, row_begin, row_end;
     } lane_miss[8] = {};
     uint32_t lane_miss_next = 0;
     unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
@@ -76,6 +79,7 @@ struct slat_ctx {
     std::unordered_map<void *, Block> live;    // allocated piece -> its extent
     std::unordered_map<void *, size_t> chunks; // hipMalloc'd base -> its size
     slat_stats stats = {};
+    slat_hostio *hio = nullptr;  // created by the first pageable host copy
 };
 
 #define SLAT_HIP(ctx, expr)                                                                        \
@@ -124,6 +128,18 @@ static inline hipError_t alloc_joint(slat_ctx *ctx, slat_csr *m, uint64_t nrows,
     m->alloc = kAllocJoint;
     return hipSuccess;
 }
+
+// Host <-> device copies of host arrays on the context's stream, synchronous (slat_hostio.hip):
+// pageable segments through the page-locked staging ring with a parallel memcpy, page-locked ones by
+// one DMA each
+struct slat_hostseg {
+    void *host;
+    void *dev;
+    size_t bytes;
+};
+slat_status slat_copy_h2d(slat_ctx *ctx, const slat_hostseg *segs, int n);
+slat_status slat_copy_d2h(slat_ctx *ctx, const slat_hostseg *segs, int n);
+void slat_hostio_destroy(slat_ctx *ctx);
 
 // workspace of at least `bytes` in ctx->ws (grown with a stream sync; contents not kept)
 slat_status slat_ensure_ws(slat_ctx *ctx, size_t bytes);

@@ -38,10 +38,7 @@ using namespace slat;
 namespace {
 
 constexpr uint32_t kLaneCap = 64;   // products per row (sort slots per lane)
-#ifndef SLAT_LANE_ROWS
-#define SLAT_LANE_ROWS 64
-#endif
-constexpr uint32_t kLaneRows = SLAT_LANE_ROWS;  // rows per one-wave block (variant builds: 32)
+constexpr uint32_t kLaneRows = 64;  // rows per one-wave block (a row per lane)
 constexpr uint32_t kLaneSeg = 256;  // A entries / products per pass (four per lane)
 #ifndef SLAT_LANE_PG
 #define SLAT_LANE_PG 4

@@ -60,15 +60,6 @@ hipError_t slat_launch_tiny(int sem, dim3 grid, size_t lds, hipStream_t s, const
 // (ell: B's ELL image; else B read in CSR form, < 2^32 entries)
 hipError_t slat_launch_symbolic_short(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
 
-// a workgroup per row (slat_group.hip): single-window launches with B in ELL form. Symbolic for every
-// value type (it reads no values); numeric for u32, Sat64 and f64 in any order (sem ids above)
-// (gt: threads per row, 128 or 256)
-hipError_t slat_launch_group_symbolic(int gt, bool idx32, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
-hipError_t slat_launch_group_numeric(int gt, int sem, bool idx32, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
-// the numeric instance's dynamic LDS for a window of ww words and `area` bytes of rank slots
-size_t slat_group_numeric_lds(uint32_t ww, uint32_t area);
-// resident 256-thread blocks per CU of the symbolic (numeric = false) or numeric instance at `lds`
-int slat_group_blocks_per_cu(int gt, int sem, bool numeric, bool idx32, size_t lds, uint32_t ww);
 
 // rows of at most slat_lane_cap() products in one kernel, a row per lane (slat_lane.hip): n rows in
 // ceil(n / 64) one-wave blocks, status = look-back words (>= the block count), maxw = max-row word;

@@ -73,14 +73,8 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #define SLAT_SAT64_NARROW 1  // Sat64 rows under the u32 bound accumulate in u32 slots (variant builds: 0)
 #endif
 
-#ifndef SLAT_BM_MERGE
-#define SLAT_BM_MERGE 0  // bitmap passes: a group's same-word columns in one atomic (variant builds: 1)
-#endif
 #ifndef SLAT_NUM_UNI
 #define SLAT_NUM_UNI 1  // k_numeric / k_numeric_short: no B-value loads for a pattern B (variant builds: 0)
-#endif
-#ifndef SLAT_ROW_PREFETCH
-#define SLAT_ROW_PREFETCH 0  // k_numeric (single-window): the next row's bounds loaded ahead (variant builds: 1)
 #endif
 #ifndef SLAT_SYM_PREFETCH
 #define SLAT_SYM_PREFETCH 1  // k_symbolic (single-window): the next row's bounds loaded ahead (variant builds: 0)
@@ -171,15 +165,25 @@ __device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.
 // word the host spins on (host_out[7]), in place of a one-thread kernel queued behind this one (a
 // dispatch of its own, ~4 us per call). Stream order still covers everything after the call; the
 // host learns of the end a few hundred ns before the grid has retired.
+// The done count is two-level (p.done: [0] groups done, [kDoneStride * (g + 1)] blocks done of group
+// g = blockIdx % 8, each word on its own 512-byte stretch): device-scope atomics on one word serialise
+// across the XCDs, ~15 ns each, so one word per block cost a 768-block launch ~10 us (C4's empty
+// window pass: 11 us); eight group words take an eighth of the blocks each, and the block that ends
+// a group adds to [0]. Every word is back at 0 when the launch has signalled.
+constexpr uint32_t kDoneStride = 64, kDoneGroups = 8;
+constexpr size_t kDoneBytes = (size_t)kDoneStride * (kDoneGroups + 1) * 8;
 __device__ __forceinline__ void signal_done(const Args &p) {
     if (p.seq == 0) return;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned long long old = __hip_atomic_fetch_add(p.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == gridDim.x - 1) {
-            __hip_atomic_store(p.done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&p.host_out[7], p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        const uint32_t G = gridDim.x, g = blockIdx.x % kDoneGroups;
+        const uint32_t groups = min(G, kDoneGroups), members = (G - g + kDoneGroups - 1) / kDoneGroups;
+        unsigned long long *gw = p.done + (size_t)kDoneStride * (g + 1);
+        if (__hip_atomic_fetch_add(gw, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != members - 1) return;
+        __hip_atomic_store(gw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add(p.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != groups - 1) return;
+        __hip_atomic_store(p.done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&p.host_out[7], p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -414,9 +418,6 @@ __device__ __forceinline__ uint32_t sat32(S v) {
 // of kOrdAhead consecutive entries are loaded before any of them is visited, so the visits (in A
 // order: the left fold of linalg/src/csr.rs:325-337) do not wait on one load chain per entry.
 constexpr int kOrdAhead = 8;
-#ifndef SLAT_ORD_DB
-#define SLAT_ORD_DB 1  // the next kOrdAhead entries' loads under this kOrdAhead's visits (variant builds: 0)
-#endif
 template <typename I, typename S, typename F>
 __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&visit) {
     const int lane = lane_id();
@@ -465,26 +466,18 @@ __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&
                 }
             });
         };
-        if constexpr (SLAT_ORD_DB) {
-            // double-buffered: the next kOrdAhead entries' loads are issued before this kOrdAhead
-            // are visited (visits stay in A order)
-            Ahead qa, qb;
-            if (cnt > 0) fetch(0, qa);
-            for (int t0 = 0; t0 < cnt; t0 += 2 * kOrdAhead) {
-                const bool hb = t0 + kOrdAhead < cnt;
-                if (hb) fetch(t0 + kOrdAhead, qb);
-                visit_all(t0, qa);
-                if (!hb) break;
-                const bool ha = t0 + 2 * kOrdAhead < cnt;
-                if (ha) fetch(t0 + 2 * kOrdAhead, qa);
-                visit_all(t0 + kOrdAhead, qb);
-            }
-        } else {
-            for (int t0 = 0; t0 < cnt; t0 += kOrdAhead) {
-                Ahead q;
-                fetch(t0, q);
-                visit_all(t0, q);
-            }
+        // double-buffered: the next kOrdAhead entries' loads are issued before this kOrdAhead
+        // are visited (visits stay in A order)
+        Ahead qa, qb;
+        if (cnt > 0) fetch(0, qa);
+        for (int t0 = 0; t0 < cnt; t0 += 2 * kOrdAhead) {
+            const bool hb = t0 + kOrdAhead < cnt;
+            if (hb) fetch(t0 + kOrdAhead, qb);
+            visit_all(t0, qa);
+            if (!hb) break;
+            const bool ha = t0 + 2 * kOrdAhead < cnt;
+            if (ha) fetch(t0 + 2 * kOrdAhead, qa);
+            visit_all(t0 + kOrdAhead, qb);
         }
     }
 }
@@ -496,30 +489,15 @@ __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&
 // B entries, the B row pointers drop out of the dependent load chain (a_col -> ELL row), and
 // rows are 16-byte aligned. Built per call into the context workspace (a few microseconds).
 // ------------------------------------------------------------------------------------------------
-// rng (row-block calls, optional): only B rows [lo, hi] are built, the column range of A's row block
-// from k_col_range ([0] (epoch << 32) | ~lo, [1] (epoch << 32) | hi; another epoch: no entries), so
-// the image's build time and bytes shrink with the block (no other B row is ever read)
 template <typename S>
 __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const uint32_t *col, const S *val,
                                                        uint32_t n, uint32_t wq, uint32_t *ecol, S *eval, uint8_t *eng,
-                                                       unsigned long long *part, const unsigned long long *rng = nullptr,
-                                                       uint32_t epoch = 0) {
+                                                       unsigned long long *part) {
     // one thread per (row k, group t): 4 columns and 4 values, written as whole groups
     // 32-bit group index: the host keeps n < 2^24 and wq <= 8 for the ELL copy
     uint32_t mx = 0, mn = 0xFFFFFFFFu;
-    uint32_t g0 = 0, total = n * wq;
-    if (rng) {
-        const unsigned long long l = rng[0], h = rng[1];
-        g0 = total = 0;
-        if ((uint32_t)(l >> 32) == epoch && (uint32_t)(h >> 32) == epoch) {
-            const uint32_t lo = ~(uint32_t)l, hi = min((uint32_t)h, n - 1);
-            if (lo <= hi) {
-                g0 = lo * wq;
-                total = (hi + 1) * wq;
-            }
-        }
-    }
-    for (uint32_t g = g0 + blockIdx.x * kBlock + threadIdx.x; g < total; g += gridDim.x * kBlock) {
+    const uint32_t total = n * wq;
+    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < total; g += gridDim.x * kBlock) {
         const uint32_t k = g / wq;
         const uint32_t t = g - k * wq;
         const uint64_t s0 = rp[k], len = rp[k + 1] - s0;
@@ -564,37 +542,6 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
                 mn = min(mn, bn[w]);
             }
             part[blockIdx.x] = ((unsigned long long)~mn << 32) | mx;
-        }
-    }
-}
-
-// the column range of A's row block [rp[0], rp[n]): rng[0] = (epoch << 32) | ~min, rng[1] = (epoch << 32) |
-// max, one atomic pair per block (k_build_ell's row range for row-block calls)
-static __global__ __launch_bounds__(kBlock) void k_col_range(const uint64_t *rp, uint64_t n, const uint32_t *col,
-                                                      unsigned long long *rng, uint32_t epoch) {
-    const uint64_t j0 = rp[0], j1 = rp[n];
-    uint32_t mx = 0, mn = 0xFFFFFFFFu;
-    for (uint64_t j = j0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < j1; j += (uint64_t)gridDim.x * kBlock) {
-        const uint32_t c = col[j];
-        mx = max(mx, c);
-        mn = min(mn, c);
-    }
-    __shared__ uint32_t bm[kBlock / kWave], bn[kBlock / kWave];
-    mx = wave_max_u32(mx);
-    mn = wave_min_u32(mn);
-    if (lane_id() == 0) {
-        bm[threadIdx.x / kWave] = mx;
-        bn[threadIdx.x / kWave] = mn;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / kWave; ++w) {
-            mx = max(mx, bm[w]);
-            mn = min(mn, bn[w]);
-        }
-        if (mn <= mx) {
-            atomicMax(&rng[0], ((unsigned long long)epoch << 32) | ~mn);
-            atomicMax(&rng[1], ((unsigned long long)epoch << 32) | mx);
         }
     }
 }
@@ -1398,39 +1345,12 @@ struct BitmapPass {
     uint32_t blk = 0;  // lane's mask of touched 64-word blocks (2048 columns each)
     __device__ __forceinline__ void operator()(uint4 c, const Quad<S> &) {
         const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
-        if constexpr (SLAT_BM_MERGE) {
-            // a group is 4 consecutive entries of a sorted B row, so columns in one bitmap word are
-            // adjacent: their bits merge into the run's first atomic (a torus row's x-1, x, x+1
-            // usually share a word), fewer ds_or and fewer same-word conflicts between them
-            uint32_t w[4], m[4];
-            bool v[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                uint32_t off = 0;
-                v[e] = win_off(cc[e], Z ? 0u : wlo, WIN, off);
-                w[e] = off >> 5;
-                m[e] = 1u << (off & 31);
-            }
-#pragma unroll
-            for (int e = 3; e > 0; --e) {
-                const bool same = v[e] && v[e - 1] && w[e] == w[e - 1];
-                m[e - 1] |= same ? m[e] : 0u;
-                v[e] = v[e] && !same;
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (v[e]) {
-                    atomicOr(&L0[w[e] * STRIDE], m[e]);
-                    blk |= 1u << (w[e] >> 6);
-                }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                uint32_t off;
-                if (win_off(cc[e], Z ? 0u : wlo, WIN, off)) {
-                    atomicOr(&L0[(off >> 5) * STRIDE], 1u << (off & 31));
-                    blk |= 1u << (off >> 11);
-                }
+        for (int e = 0; e < 4; ++e) {
+            uint32_t off;
+            if (win_off(cc[e], Z ? 0u : wlo, WIN, off)) {
+                atomicOr(&L0[(off >> 5) * STRIDE], 1u << (off & 31));
+                blk |= 1u << (off >> 11);
             }
         }
     }
@@ -1803,44 +1723,12 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
     const bool dyn = MODE != 0 && p.tq != nullptr;  // launch-uniform (single-window passes: a fixed stride)
     const TicketQueue tq(p.tq, nit, stride);
     unsigned long long pend = 0;
-    // (SLAT_ROW_PREFETCH, single-window passes) the next row's bounds, C offsets and stored block mask
-    // loaded by lanes 0-4 while this row runs: one dependent latency less per row
-    constexpr bool kPre = SLAT_ROW_PREFETCH && MODE == 0;
-    uint64_t pre = 0;
-    auto prefetch = [&](uint64_t r) {
-        if constexpr (kPre) {
-            if (r < nit) {
-                if (lane < 2)
-                    pre = p.a_rp[r + lane];
-                else if (lane < 4)
-                    pre = p.c_rp[r + lane - 2];
-                else if (lane == 4 && p.smask)
-                    pre = p.smask[r];
-            }
-        }
-    };
-    prefetch(first);
     for (uint64_t it = first; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
         if (dyn) pend = tq.issue();
         const uint64_t row = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(p.list[it]) : it;
-        I a0, a1;
-        uint64_t out_begin, out_end;
-        uint32_t pmask = 0;
-        if constexpr (kPre) {
-            a0 = (I)readlane_u64(pre, 0);
-            a1 = (I)readlane_u64(pre, 1);
-            out_begin = readlane_u64(pre, 2);
-            out_end = readlane_u64(pre, 3);
-            pmask = (uint32_t)readlane_u64(pre, 4);
-            prefetch(it + stride);
-        }
         if (fat_row(p, row)) continue;  // the fat-row kernels' row
-        if constexpr (!kPre) {
-            a0 = (I)p.a_rp[row];
-            a1 = (I)p.a_rp[row + 1];
-            out_begin = p.c_rp[row];
-            out_end = p.c_rp[row + 1];
-        }
+        const I a0 = (I)p.a_rp[row], a1 = (I)p.a_rp[row + 1];
+        const uint64_t out_begin = p.c_rp[row], out_end = p.c_rp[row + 1];
         uint64_t out_pos = out_begin;
         uint32_t zeros = 0;
         ph[kPhaseSlots - 1] += 1;
@@ -1949,7 +1837,7 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
                     //     at a time, ranked from registers and written whole ({bits, rank} per word),
                     //     so untouched blocks may hold stale words (no valid column reads them) and
                     //     nothing is cleared afterwards
-                    bmask = kPre ? pmask : __builtin_amdgcn_readfirstlane(p.smask[row]);
+                    bmask = __builtin_amdgcn_readfirstlane(p.smask[row]);
                     const uint32_t *src = p.sbm + row * ((uint64_t)p.nblk * kWave) + lane;
                     uint32_t m = bmask;
                     while (m) {
@@ -2849,37 +2737,6 @@ constexpr int kScanThreads = SLAT_SCAN_THREADS, kScanItems = SLAT_SCAN_ITEMS;
 constexpr uint64_t kScanTile = (uint64_t)kScanThreads * kScanItems;
 constexpr unsigned long long kStAgg = 1ull << 40, kStInc = 2ull << 40, kStVal = (1ull << 40) - 1;
 
-// One lane: publish tile `tile`'s aggregate, walk back over the earlier tiles' status words (tags of
-// this epoch: an aggregate, or an inclusive prefix that ends the walk) and publish the tile's own
-// inclusive prefix; returns its exclusive prefix. Tiles are taken in ticket order, so every earlier
-// tile belongs to a block that is running or done and never waits on a later one.
-__device__ __forceinline__ unsigned long long lookback_prefix(unsigned long long *status, uint64_t tile, uint32_t epoch,
-                                                              unsigned long long agg) {
-    auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto st = [](unsigned long long *x, unsigned long long v) {
-        __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    const unsigned long long tag = (unsigned long long)epoch << 42;
-    unsigned long long excl = 0;
-    if (tile == 0) {
-        st(&status[0], tag | kStInc | agg);
-        return 0;
-    }
-    st(&status[tile], tag | kStAgg | agg);
-    for (uint64_t j = tile - 1;; --j) {
-        unsigned long long x;
-        while (true) {
-            x = ld(&status[j]);
-            if ((x >> 42) == epoch && (x & (kStAgg | kStInc)) != 0) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        excl += x & kStVal;
-        if (x & kStInc) break;
-    }
-    st(&status[tile], tag | kStInc | (excl + agg));
-    return excl;
-}
-
 __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long long v) {
     const int lane = lane_id();
 #pragma unroll
@@ -2890,9 +2747,13 @@ __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long l
     return v;
 }
 
-// The same protocol by a whole wave: lane j reads tile - 1 - j, so one round covers 64 predecessors
-// (the nearest inclusive prefix by ballot, the aggregates before it by a wave sum) instead of one
-// dependent load per predecessor. Many small tiles arriving together (k_lane: ~400 one-wave blocks)
+// Decoupled look-back by a whole wave: publish tile `tile`'s aggregate, then walk back over the
+// earlier tiles' epoch-tagged status words (an aggregate, or an inclusive prefix that ends the walk)
+// and publish the tile's own inclusive prefix; returns its exclusive prefix. Tiles are taken in
+// ticket (or resident block) order, so every earlier tile belongs to a block that is running or
+// done and never waits on a later one. Lane j reads tile - 1 - j, so one round covers 64
+// predecessors (the nearest inclusive prefix by ballot, the aggregates before it by a wave sum)
+// instead of one dependent load per predecessor. Many small tiles arriving together (k_lane: ~400 one-wave blocks)
 // made the lane-0 walk a chain of hundreds of loads. Called by every lane of the wave; returns the
 // tile's exclusive prefix in every lane.
 // (split in two: lookback_publish stores the tile's aggregate (tile 0: its inclusive prefix), and
@@ -3003,15 +2864,18 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
         wpre += k < w ? x : 0ull;
         agg += x;
     }
-    if (t == 0) {
+    if (w == 0) {
         uint32_t m = 0;
         for (int k = 0; k < kScanThreads / kWave; ++k) m = max(m, wmax[k]);
         // max row first (its result waited for), then the status: the max is in place once any
         // later tile sees this tile's status (bmax: the last tile has it from the producer's maxima)
-        if (!bmax) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
-        const unsigned long long excl = lookback_prefix(status, tile, epoch, agg);
-        s_bcast[1] = excl;
-        if (tile == ntiles - 1) {
+        if (!bmax && lane == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
+        // the walk by the whole wave, 64 predecessors per round: a lane-0 walk was one dependent
+        // load per predecessor still holding only its aggregate (one rank's eighth of C4, 62 tiles:
+        // 18.8 us for a 1 MB scan)
+        const unsigned long long excl = lookback_prefix_wave(status, tile, epoch, agg);
+        if (lane == 0) s_bcast[1] = excl;
+        if (lane == 0 && tile == ntiles - 1) {
             if (n > 0) rp[0] = 0;
             const unsigned long long mw = bmax ? 0ull : ld(maxw);
             const unsigned long long out[2] = {excl + agg, bmax ? (unsigned long long)m

@@ -313,11 +313,10 @@ def test_rowblock_partition_concatenates_to_full(ctx):
 
 
 @pytest.mark.parametrize("dtype", [slat.U32, slat.SAT64, slat.F64])
-def test_rowblock_ell_built_over_referenced_rows(ctx, dtype):
-    # row blocks of A^3 * A take B's ELL image built only over the B rows the block's columns reach
-    # (k_col_range -> k_build_ell's row range): one-row blocks, the first and last rows (the range at
-    # either end of B), a middle stretch, and blocks in both orders on one context (stale ranges of an
-    # earlier call must not leak into the next)
+def test_rowblock_slices_of_full_product(ctx, dtype):
+    # row blocks of A^3 * A through the pipeline (B in its ELL image): one-row blocks, the first and
+    # last rows, a middle stretch, and blocks in both orders on one context (nothing of an earlier
+    # call's workspace may leak into the next); each block is the full product's row slice
     a = O.torus_thinned(16, 3.0, O.Rng())
     a3 = O.matmul_seq(O.matmul_seq(a, a), a)
     full = O.matmul_seq(a3, a)
