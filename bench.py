@@ -186,6 +186,22 @@ def timed_steps(run, steps, warmup, barrier):
     return time.perf_counter() - t0
 
 
+def c1_leg(ctx, A, steps: int, warmup: int, side: int):
+    """The metric's literal config C1 (README.md:41): C = A * A on the same torus, timed like the headline
+    (full synchronous calls, device-resident operands, the output released inside the call), plus the
+    golden check of one output."""
+    nz = [0]
+
+    def run():
+        C = A.matmul(A)
+        nz[0] = C.nnz()
+        del C
+
+    el = timed_steps(run, steps, warmup, ctx.sync)
+    return {"c1_ms_per_call": round(el / steps * 1e3, 4), "c1_gnnz_per_s": round(nz[0] * steps / el / 1e9, 4),
+            "c1_parity": parity(A.matmul(A), side, 2)}
+
+
 def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
     """North_star strong scaling on config C4 (100^3 torus, C = A^3 * A): flops-balanced row blocks
     over the ranks, B and the left operand broadcast from rank 0; then the blocks' allgatherv over
@@ -200,6 +216,12 @@ def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
     n = A.n
     cuts = slat_dist.device_cuts(P, A, world) if world > 1 else [0, n]
     lo, hi = cuts[rank], cuts[rank + 1]
+    # the replicated B prepared once with the broadcast (its ELL image and value summary,
+    # slat_bprep_create), timed apart as prep_ms; the rank's blocks and the single-GPU anchor both use it
+    ctx.sync()
+    tp = time.perf_counter()
+    B = A.prepare()
+    prep_ms = (time.perf_counter() - tp) * 1e3
 
     def barrier():
         if dist is not None:
@@ -209,7 +231,7 @@ def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
     nz = [0]
 
     def run():
-        C = P.matmul_rowblock(lo, hi, A, 0)
+        C = P.matmul_rowblock(lo, hi, B, 0)
         nz[0] = C.nnz()
         del C
 
@@ -225,11 +247,12 @@ def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
         el, units = float(tm[0].item()), int(t[1].item())
     out = {"workload": "100^3 Moore torus thinned to 3 e/n (seed [42;32]), C = A^3 * A, u32 (config C4)",
            "n_gpus": world, "rows": [lo, hi], "cuts": cuts if world <= 16 else None,
-           "ms_per_step": round(el / steps * 1e3, 4), "gnnz_per_s": round(units / el / 1e9, 4)}
+           "ms_per_step": round(el / steps * 1e3, 4), "gnnz_per_s": round(units / el / 1e9, 4),
+           "prep_ms": round(prep_ms, 4)}
     # the blocks assembled over RCCL (every rank), checked against the golden digests on rank 0
     par = None
     if comm is not None:  # RCCL (also at world size 1 under SLAT_FORCE_DIST)
-        C = P.matmul_rowblock(lo, hi, A, 0)
+        C = P.matmul_rowblock(lo, hi, B, 0)
         comm.allgather_rows(C)  # warm-up (RCCL connection setup)
         dist.barrier()
         tg = time.perf_counter()
@@ -242,7 +265,7 @@ def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
     elif dist is not None:
         # gloo rehearsal (ranks sharing a GPU, no RCCL): the blocks assembled on the host
         # (slat.dist.gather_blocks, the allgatherv restated over torch.distributed) and checked on rank 0
-        C = P.matmul_rowblock(lo, hi, A, 0)
+        C = P.matmul_rowblock(lo, hi, B, 0)
         h = C.host()
         del C
         rp, col, val = slat_dist.gather_blocks(h.row_ptr, h.col_idx, h.values)
@@ -250,7 +273,7 @@ def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
             par = parity_arrays(rp, col, val, side, power)
         del rp, col, val, h
     elif world == 1:
-        C = P.matmul_rowblock(0, n, A, 0)
+        C = P.matmul_rowblock(0, n, B, 0)
         par = parity(C, side, power)
         del C
     out["parity"] = par
@@ -262,7 +285,7 @@ def c4_leg(ctx, dist, comm, rank, world, steps, warmup):
             single = el / steps * 1e3
         else:
             def one():
-                C1 = P.matmul_rowblock(0, n, A, 0)
+                C1 = P.matmul_rowblock(0, n, B, 0)
                 del C1
             single = timed_steps(one, max(5, min(steps, 20)), 3, ctx.sync) / max(5, min(steps, 20)) * 1e3
         out["single_gpu_ms"] = round(single, 4)
@@ -373,6 +396,7 @@ def main():
         ok = torch.tensor([0 if par is False else 1], dtype=torch.int32, device=coll_dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     nnz_a = P.nnz()
+    c1 = c1_leg(ctx, A, args.steps, args.warmup, side) if rank == 0 else None
     e2e = e2e_leg(ctx, P, A, args.e2e_steps) if (rank == 0 and args.e2e_steps > 0) else None
     del P
 
@@ -383,14 +407,14 @@ def main():
         comm.close()
     if rank == 0:
         emit(args, world, side, power, n, nnz_a, A.nnz(), nnz_c, value, ms_per_step, stats, sym, scan, num, tot, abl, par, c4,
-             e2e)
+             e2e, c1)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 
 
 def emit(args, world, side, power, n, nnz_a, nnz_b, nnz_c, value, ms_per_step, stats, sym, scan, num, tot, abl, par, c4,
-         e2e=None):
+         e2e=None, c1=None):
     alg = algorithmic_bytes(nnz_a, nnz_b, nnz_c, n, 4)
     num_ms = float(np.mean(num))
     achieved = alg / (max(num_ms, 1e-6) * 1e-3) / 1e9
@@ -423,11 +447,14 @@ def emit(args, world, side, power, n, nnz_a, nnz_b, nnz_c, value, ms_per_step, s
                    "capacity": stats["capacity"], "mode": stats["mode"], "window_words": stats["window_words"],
                    **({"ablated_ms": round(float(np.mean(abl)), 4)} if os.environ.get("SLAT_ABLATE") else {}),
                    **({"c4": c4} if c4 is not None else {}),
+                   # the metric's literal A x A (config C1), timed like the headline
+                   **(c1 or {}),
                    # the C4 strong-scaling figures again as top-level scalars (a nested dict may not
                    # survive a flat parse of the line)
                    **({"c4_ms_per_step": c4.get("ms_per_step"), "c4_gnnz_per_s": c4.get("gnnz_per_s"),
                        "c4_single_gpu_ms": c4.get("single_gpu_ms"), "c4_speedup": c4.get("speedup"),
-                       "c4_gather_ms": c4.get("gather_ms"), "c4_parity": c4.get("parity")} if c4 is not None else {}),
+                       "c4_gather_ms": c4.get("gather_ms"), "c4_parity": c4.get("parity"),
+                       "c4_prep_ms": c4.get("prep_ms")} if c4 is not None else {}),
                    # host-resident calls (PCIe both ways: the drop-in's cost for Vec in / Vec out)
                    **({"e2e_ms": round(e2e["pageable"][0], 4), "e2e_gnnz_per_s": round(e2e["pageable"][1], 4),
                        "e2e_pinned_ms": round(e2e["pinned"][0], 4),
@@ -435,6 +462,12 @@ def emit(args, world, side, power, n, nnz_a, nnz_b, nnz_c, value, ms_per_step, s
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    # north_star's strong scaling as a top-level series: config C4 split over the N ranks (at N = 1 the
+    # whole product on one GPU), all ranks' output nnz / the max-over-ranks time; the driver's 1/2/4/8
+    # runs give the strong-scaling curve from these values (value itself stays the headline workload)
+    if c4 is not None:
+        out["scaling_value"] = c4.get("gnnz_per_s")
+        out["scaling_metric"] = "GNNZ/s for A^3×A on 100³ Moore torus (config C4), rows split over n_gpus (strong)"
     print(json.dumps(out), flush=True)
 
 

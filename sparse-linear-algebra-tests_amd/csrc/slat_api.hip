@@ -601,8 +601,32 @@ static hipError_t wait_stream(slat_ctx *ctx, hipStream_t s, unsigned long long s
     return hipSuccess;
 }
 
+// B's padded ELL image applies: short rows (<= 32 entries), a bounded blow-up, 24-bit row indices and
+// 31-bit byte offsets in the kernels
+static bool ell_fits(const slat_csr_view *B, uint64_t maxrow_b, size_t vs) {
+    const uint64_t q = (maxrow_b + 3) / 4;
+    const uint64_t bytes = B->n_rows * q * 4 * (4 + vs);
+    return maxrow_b <= 32 && bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
+           B->n_rows < (1ull << 24) && B->n_rows * q * 16 * (vs / 4) < (1ull << 31);
+}
+
+static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin, uint64_t row_end,
+                                 const slat_csr_view *B, const slat_bprep *prep, slat_csr *C, uint32_t flags);
+
 extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
                                             uint64_t row_end, const slat_csr_view *B, slat_csr *C, uint32_t flags) {
+    return rowblock_impl(ctx, A, row_begin, row_end, B, nullptr, C, flags);
+}
+
+extern "C" slat_status slat_spgemm_rowblock_prepared(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin,
+                                                     uint64_t row_end, const slat_bprep *B, slat_csr *C, uint32_t flags) {
+    if (!ctx || !B) return SLAT_EINVAL;
+    if (B->device != ctx->device) return fail(ctx, SLAT_EINVAL, "prepared B belongs to another device");
+    return rowblock_impl(ctx, A, row_begin, row_end, &B->b, B, C, flags);
+}
+
+static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t row_begin, uint64_t row_end,
+                                 const slat_csr_view *B, const slat_bprep *prep, slat_csr *C, uint32_t flags) {
     if (!ctx || !C) return SLAT_EINVAL;
     HostClock hc;
     hc.start();
@@ -631,7 +655,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
             vb = slat_csr_view_of(&dB);
             pb = &vb;
         }
-        st = slat_spgemm_rowblock(ctx, pa, row_begin, row_end, pb, C, flags);
+        st = rowblock_impl(ctx, pa, row_begin, row_end, pb, nullptr, C, flags);
         if (dA.row_ptr) slat_csr_free(ctx, &dA);
         if (dB.row_ptr) slat_csr_free(ctx, &dB);
         return st;
@@ -658,7 +682,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         return SLAT_OK;
     }
-    uint64_t maxrow_b = B->max_row_nnz;
+    uint64_t maxrow_b = prep ? prep->maxrow_b : B->max_row_nnz;
     if (maxrow_b == 0 && (st = slat_csr_max_row_nnz(ctx, B, &maxrow_b))) return st;
     // C's capacity by the exact bound nnz(A block) x max row(B) (no mid-call sync) unless it exceeds
     // the budget: free device memory / 4 (re-read when this context's pool grew or shrank, else every
@@ -729,7 +753,6 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     // windows (mode 2; numeric windows of 1024 words keep two blocks per CU).
     // padded ELL copy of B when its rows are short (bounded blow-up)
     const uint64_t wq = (maxrow_b + 3) / 4;
-    const uint64_t ell_bytes = B->n_rows * wq * 4 * (4 + vs);
     // small products: the whole call in one regular launch (slat_tiny.hip) — one window of at most
     // 8192 columns, <= 2048 rows (at 3375 rows, the 15^3 cells, it measured 1-2 us slower than the
     // pipeline: profiles/r03_small_cells_tiny_abi.csv), 32-bit offsets, a wave per row with every row in flight, a product bound a wave
@@ -759,9 +782,9 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                 m.row_end == row_end)
                 lane = false;
     static const bool kNoEll = slat_ab_knob("SLAT_NO_ELL") != nullptr;
-    const bool ell = maxrow_b <= 32 && ell_bytes <= std::max<uint64_t>(64ull << 20, 8 * B->nnz * (4 + vs)) &&
-                     B->n_rows < (1ull << 24) && B->n_rows * wq * 16 * (vs / 4) < (1ull << 31) &&
-                     !kNoEll && !tiny && !lane;  // 24-bit row index, 31-bit byte offsets in the kernels
+    const bool ell = ell_fits(B, maxrow_b, vs) && !kNoEll && !tiny && !lane;
+    // a prepared B (slat_bprep_create) brings its image and value summary: no per-call build
+    const bool pell = ell && prep && prep->ell && prep->wq == wq;
     // stored bitmaps (single-window launches): symbolic keeps each row's touched bitmap blocks for
     // numeric, n * ww words at most (only touched blocks are written), capped against free memory
     const uint64_t sbm_words = a.wide ? 0 : (uint64_t)n * a.ww;
@@ -880,8 +903,9 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     auto up256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t counts_b = up256(n * 8);
     const size_t shards_b = 4096 + (SLAT_PHASES ? 8192 : 0);  // + phase-timing slots (diagnostic builds)
-    const size_t ecol_b = ell ? up256(B->n_rows * wq * 16) : 0, eval_b = ell ? up256(B->n_rows * wq * 4 * vs) : 0;
-    const size_t eng_b = ell ? up256(B->n_rows) : 0;
+    const bool bell = ell && !pell;  // the image built by this call
+    const size_t ecol_b = bell ? up256(B->n_rows * wq * 16) : 0, eval_b = bell ? up256(B->n_rows * wq * 4 * vs) : 0;
+    const size_t eng_b = bell ? up256(B->n_rows) : 0;
     const size_t sbm_b = sbm ? up256(sbm_words * 4) : 0, smask_b = sbm ? up256(n * 4) : 0;
     const size_t o_abl = counts_b, o_sh = o_abl + counts_b, o_ecol = o_sh + shards_b,
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
@@ -895,13 +919,22 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     const uint64_t fat_min = slat_fat_min(!ell && (dt != SLAT_F64 || f64any));
     const bool fat = !kNoFat && !tiny && !lane && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= fat_min : maxrow_b > 32);
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
-    const size_t o_part = o_lc + lc_b, part_b = (ell && dt != SLAT_F64) ? 4096 * 8 : 0;
+    const size_t o_part = o_lc + lc_b, part_b = (bell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
     const size_t o_bmax = o_fat + fat_b,  // per-block max counts (the symbolic grid)
         bmax_b = up256((size_t)std::max<uint64_t>(sym_grid.x, (uint64_t)ctx->cu_count * 8) * 4);
     if ((st = slat_ensure_ws(ctx, o_bmax + bmax_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
-    if (ell) {
+    if (pell) {
+        a.ell_wq = (uint32_t)wq;
+        a.ell_col = prep->ecol;
+        a.ell_val = prep->eval;
+        a.ell_ng = prep->eng;
+        if (dt != SLAT_F64) {  // the prepared summary, tagged with its own epoch
+            a.b_vmax = prep->vmax;
+            a.epoch = prep->epoch;
+        }
+    } else if (ell) {
         a.ell_wq = (uint32_t)wq;
         a.ell_col = (const uint32_t *)(ws + o_ecol);
         a.ell_val = ws + o_eval;
@@ -928,7 +961,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     hc.mark(2);
     // the ELL image (or B's value summary) first: it runs while the host allocates C and queues
     // the rest, instead of after the host's setup with the GPU idle
-    if (ell) {
+    if (bell) {
         hipError_t be;
         if (dt == SLAT_U32)
             be = launch_build_ell<uint32_t>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng,
@@ -1049,7 +1082,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
                                                          B->nnz,     A->n_rows,   row_begin, row_end};
             // a row of more than slat_lane_cap() products: the call through the pipeline
             (void)failc(SLAT_OK);
-            return slat_spgemm_rowblock(ctx, A, row_begin, row_end, B, C, flags | SLAT_FLAG_NO_TINY);
+            return rowblock_impl(ctx, A, row_begin, row_end, B, prep, C, flags | SLAT_FLAG_NO_TINY);
         }
     } else {
     if (a.stats || SLAT_PHASES) SLAT_HIPC(hipMemsetAsync(a.shards, 0, shards_b, s));
@@ -1129,7 +1162,7 @@ extern "C" slat_status slat_spgemm_rowblock(slat_ctx *ctx, const slat_csr_view *
     hc.mark(5);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
     // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
-    const bool bpart = ell && dt != SLAT_F64;
+    const bool bpart = bell && dt != SLAT_F64;
     if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
                                bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
                                bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch, asym.bmax, sym_blocks)))
@@ -1313,4 +1346,72 @@ extern "C" slat_status slat_spgemm_csr_sat64(slat_ctx *ctx, const slat_csr_view 
 extern "C" slat_status slat_spgemm_csr_f64(slat_ctx *ctx, const slat_csr_view *A, const slat_csr_view *B, slat_csr *C,
                                            uint32_t flags) {
     return typed(ctx, A, B, C, flags, SLAT_F64);
+}
+
+// ---------------------------------------------------------------------------------------------
+// A prepared right operand: B's padded ELL image and its clamped value summary, built once for many
+// products with the same B (the replicated B of the multi-GPU row blocks, an A^k chain's A)
+// ---------------------------------------------------------------------------------------------
+extern "C" slat_status slat_bprep_create(slat_ctx *ctx, const slat_csr_view *B, slat_bprep **out) {
+    if (!ctx || !out) return SLAT_EINVAL;
+    *out = nullptr;
+    slat_status st = slat_check_view(ctx, B, "B");
+    if (st) return st;
+    if (B->residency != SLAT_DEVICE) return fail(ctx, SLAT_EINVAL, "a prepared B must be device-resident");
+    SLAT_HIP(ctx, hipSetDevice(ctx->device));
+    slat_bprep *p = new slat_bprep();
+    p->b = *B;
+    p->device = ctx->device;
+    uint64_t mr = B->max_row_nnz;
+    if (mr == 0 && B->n_rows && (st = slat_csr_max_row_nnz(ctx, B, &mr))) {
+        delete p;
+        return st;
+    }
+    p->maxrow_b = mr;
+    p->b.max_row_nnz = mr;
+    const size_t vs = vsize(B->dtype);
+    p->wq = (uint32_t)((mr + 3) / 4);
+    p->ell = mr > 0 && B->nnz > 0 && ell_fits(B, mr, vs);
+    if (p->ell) {
+        hipStream_t s = ctx->stream;
+        const uint32_t nparts = build_ell_blocks(B, p->wq);
+        unsigned long long *parts = nullptr;
+        hipError_t e = slat_dev_alloc(ctx, (void **)&p->ecol, B->n_rows * p->wq * 16, s);
+        if (e == hipSuccess) e = slat_dev_alloc(ctx, &p->eval, B->n_rows * p->wq * 4 * vs, s);
+        if (e == hipSuccess) e = slat_dev_alloc(ctx, (void **)&p->eng, B->n_rows, s);
+        if (e == hipSuccess) e = slat_dev_alloc(ctx, (void **)&p->vmax, 64, s);
+        if (e == hipSuccess && B->dtype != SLAT_F64) e = slat_dev_alloc(ctx, (void **)&parts, (size_t)nparts * 8, s);
+        if (e == hipSuccess) {
+            if (B->dtype == SLAT_U32)
+                e = launch_build_ell<uint32_t>(s, B, p->wq, p->ecol, p->eval, p->eng, parts);
+            else if (B->dtype == SLAT_SAT64)
+                e = launch_build_ell<unsigned long long>(s, B, p->wq, p->ecol, p->eval, p->eng, parts);
+            else
+                e = launch_build_ell<double>(s, B, p->wq, p->ecol, p->eval, p->eng, nullptr);
+        }
+        p->epoch = 1;
+        if (e == hipSuccess && parts) {
+            hipLaunchKernelGGL(k_reduce_bparts, dim3(1), dim3(kWave), 0, s, parts, nparts, p->vmax, p->epoch);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (parts) slat_dev_free(ctx, parts, s);
+        if (e != hipSuccess) {
+            ctx->err = std::string("slat_bprep_create: ") + hipGetErrorString(e);
+            (void)slat_bprep_free(ctx, p);
+            return SLAT_EHIP;
+        }
+    }
+    *out = p;
+    return SLAT_OK;
+}
+
+extern "C" slat_status slat_bprep_free(slat_ctx *ctx, slat_bprep *p) {
+    if (!ctx) return SLAT_EINVAL;
+    if (!p) return SLAT_OK;
+    (void)hipSetDevice(ctx->device);
+    for (void *q : {(void *)p->ecol, p->eval, (void *)p->eng, (void *)p->vmax})
+        if (q) slat_dev_free(ctx, q, ctx->stream);
+    delete p;
+    return SLAT_OK;
 }

@@ -82,6 +82,21 @@ struct slat_ctx {
     slat_hostio *hio = nullptr;  // created by the first pageable host copy
 };
 
+// A prepared right operand (slat_bprep_create): the borrowed view, its max row, and (ell) the padded
+// ELL image with the clamped B-value summary words vmax[kVMaxWord] / [kVMinInvWord] tagged `epoch`
+struct slat_bprep {
+    slat_csr_view b;
+    uint64_t maxrow_b = 0;
+    uint32_t wq = 0;
+    bool ell = false;
+    uint32_t *ecol = nullptr;
+    void *eval = nullptr;
+    uint8_t *eng = nullptr;
+    unsigned long long *vmax = nullptr;
+    uint32_t epoch = 0;
+    int device = 0;
+};
+
 #define SLAT_HIP(ctx, expr)                                                                        \
     do {                                                                                           \
         hipError_t e_ = (expr);                                                                    \

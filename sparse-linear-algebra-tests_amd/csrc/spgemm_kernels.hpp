@@ -546,6 +546,24 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
     }
 }
 
+// k_build_ell's per-block partials ((~min << 32) | max) reduced by one wave into vmax[kVMaxWord] =
+// (epoch << 32) | max and vmax[kVMinInvWord] = (epoch << 32) | ~min (a prepared B's summary)
+static __global__ __launch_bounds__(kWave) void k_reduce_bparts(const unsigned long long *part, uint32_t n,
+                                                                unsigned long long *vmax, uint32_t epoch) {
+    uint32_t bx = 0, bn = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += kWave) {
+        const unsigned long long q = part[i];
+        bx = max(bx, (uint32_t)q);
+        bn = max(bn, (uint32_t)(q >> 32));
+    }
+    bx = wave_max_u32(bx);
+    bn = wave_max_u32(bn);
+    if (threadIdx.x == 0) {
+        vmax[kVMaxWord] = ((unsigned long long)epoch << 32) | bx;
+        vmax[kVMinInvWord] = ((unsigned long long)epoch << 32) | bn;
+    }
+}
+
 // the same B-value summary when B is walked in CSR form (no ELL copy): max and ~min of the u32
 // values, epoch-tagged, one atomic pair per block
 template <typename S>

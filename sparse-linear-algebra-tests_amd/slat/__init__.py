@@ -6,12 +6,12 @@ CsrMatrix.matmul / matmul_par (src/graph_csr.rs:306-484), MagnusMatrix.matmul / 
 """
 from ._lib import (DEVICE, F64, FLAG_EXACT_ALLOC, FLAG_F64_ANY_ORDER, FLAG_FAT_BUCKETS, FLAG_IDX64, FLAG_NO_TINY, FLAG_STATS, FLAG_TIMING, HOST, SAT64, U32, SlatError, build,
                    lib)
-from .matrix import (Context, Csr, CsrBTreeMatrix, CsrF64, CsrMatrix, CsrU32, CsrU64, DeviceCsr, HostCsr, MagnusMatrix, MagnusMatrixUsize, StdRng,
+from .matrix import (Context, Csr, CsrBTreeMatrix, CsrF64, CsrMatrix, CsrU32, CsrU64, DeviceCsr, HostCsr, MagnusMatrix, MagnusMatrixUsize, PreparedB, StdRng,
                      default_context, host_from_coo, host_lattice, host_random, host_rmat, host_thin, load_edges, pinned_empty, spgemm_host,
                      torus_thinned, torus_thinned_device)
 
 __all__ = [
-    "Context", "Csr", "CsrBTreeMatrix", "CsrF64", "CsrMatrix", "CsrU32", "CsrU64", "DeviceCsr", "HostCsr", "MagnusMatrix", "MagnusMatrixUsize", "StdRng",
+    "Context", "Csr", "CsrBTreeMatrix", "CsrF64", "CsrMatrix", "CsrU32", "CsrU64", "DeviceCsr", "HostCsr", "MagnusMatrix", "MagnusMatrixUsize", "PreparedB", "StdRng",
     "default_context", "host_from_coo", "host_lattice", "host_random", "host_rmat", "host_thin", "load_edges", "pinned_empty", "spgemm_host", "torus_thinned", "torus_thinned_device", "SlatError",
     "build", "lib", "U32", "SAT64", "F64", "DEVICE", "HOST", "FLAG_TIMING", "FLAG_EXACT_ALLOC", "FLAG_STATS", "FLAG_F64_ANY_ORDER", "FLAG_IDX64", "FLAG_NO_TINY", "FLAG_FAT_BUCKETS",
     "set_matmul_progress",

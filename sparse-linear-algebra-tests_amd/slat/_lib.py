@@ -33,7 +33,7 @@ EXPORTS = [
     "slat_magnus_connected_components",
     "slat_comm_id", "slat_comm_create", "slat_comm_destroy", "slat_rowblock_cuts", "slat_bcast_csr",
     "slat_allgather_rows", "slat_concat_rows", "slat_diameter", "slat_spgemm_btree", "slat_host_alloc",
-    "slat_host_free",
+    "slat_host_free", "slat_bprep_create", "slat_bprep_free", "slat_spgemm_rowblock_prepared",
 ]
 
 
@@ -180,6 +180,9 @@ def lib():
         "slat_spgemm_btree": ([vp, P(BTreeView), P(BTreeView), P(CsrOwned), u32], C.c_int),
         "slat_host_alloc": ([u64, P(vp)], C.c_int),
         "slat_host_free": ([vp], C.c_int),
+        "slat_bprep_create": ([vp, P(CsrView), P(vp)], C.c_int),
+        "slat_bprep_free": ([vp, vp], C.c_int),
+        "slat_spgemm_rowblock_prepared": ([vp, P(CsrView), u64, u64, vp, P(CsrOwned), u32], C.c_int),
     }
     for name, (args, res) in sig.items():
         if os.environ.get("SLAT_LIB_PATH") and not hasattr(L, name):

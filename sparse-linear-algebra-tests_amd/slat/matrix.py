@@ -561,12 +561,46 @@ class DeviceCsr:
         L.check(L.lib().slat_csr_create(self._ctx.ptr, C.byref(v), C.byref(out)), self._ctx.ptr)
         return type(self)(out, self._ctx)
 
-    def matmul_rowblock(self, row_begin: int, row_end: int, other: "DeviceCsr", flags: int = 0):
-        a, b = self._cview(), other._cview()
+    def matmul_rowblock(self, row_begin: int, row_end: int, other, flags: int = 0):
+        """Rows [row_begin, row_end) of self * other (slat_spgemm_rowblock); `other` may be a
+        PreparedB of the right operand (slat_spgemm_rowblock_prepared: its ELL image built once)."""
+        a = self._cview()
         out = L.CsrOwned()
-        L.check(L.lib().slat_spgemm_rowblock(self._ctx.ptr, C.byref(a), row_begin, row_end, C.byref(b),
-                                             C.byref(out), flags), self._ctx.ptr)
+        if isinstance(other, PreparedB):
+            if other.dtype != self.DTYPE:
+                raise TypeError("operands must have the same value type")
+            L.check(L.lib().slat_spgemm_rowblock_prepared(self._ctx.ptr, C.byref(a), row_begin, row_end, other.ptr,
+                                                          C.byref(out), flags), self._ctx.ptr)
+        else:
+            b = other._cview()
+            L.check(L.lib().slat_spgemm_rowblock(self._ctx.ptr, C.byref(a), row_begin, row_end, C.byref(b),
+                                                 C.byref(out), flags), self._ctx.ptr)
         return type(self)(out, self._ctx)
+
+    def prepare(self) -> "PreparedB":
+        """This matrix as a prepared right operand (slat_bprep_create)."""
+        return PreparedB(self)
+
+
+class PreparedB:
+    """A right operand prepared once (slat_bprep_create: B's padded ELL image and value summary) for
+    many row-block products; holds a reference to the matrix, whose arrays it borrows."""
+
+    def __init__(self, m: DeviceCsr):
+        self._m = m
+        self._ctx = m._ctx
+        self.dtype = m.DTYPE
+        self.ptr = C.c_void_p()
+        v = m._cview()
+        L.check(L.lib().slat_bprep_create(self._ctx.ptr, C.byref(v), C.byref(self.ptr)), self._ctx.ptr)
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                L.lib().slat_bprep_free(self._ctx.ptr, self.ptr)
+                self.ptr = C.c_void_p()
+        except Exception:
+            pass
 
 
 class CsrMatrix(DeviceCsr):
