@@ -18,7 +18,7 @@
 //      wave's longest row decides; the values stay in LDS, found by the slot in the key) and counts
 //      its distinct columns;
 //   4. the wave's offset by a decoupled look-back over the earlier waves' status words (one wave per
-//      block; lookback_prefix_wave reads 64 predecessors per round), then row_ptr, and the rows'
+//      block; lookback_walk reads 256 predecessors per round), then row_ptr, and the rows'
 //      sums in key order — the f64 left fold from 0.0 in A order, the saturating integer sums — are
 //      stored; zero sums (explicit zero inputs, f64 cancellation) are counted for the host's
 //      compaction, as after k_numeric. The last block stores

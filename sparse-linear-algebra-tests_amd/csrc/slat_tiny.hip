@@ -7,7 +7,7 @@
 //   1. the row's column bitmap and word ranks in LDS (numeric's steps 1-2: B walked in CSR form, no
 //      ELL image to build); the rank total IS the row's structural count;
 //   2. the block's counts summed in LDS, then the block's offset by a decoupled look-back over the
-//      earlier blocks' epoch-tagged status words (lookback_prefix_wave: the first wave reads 64
+//      earlier blocks' epoch-tagged status words (lookback_prefix_wave: the first wave reads 256
 //      predecessors per round) — no grid
 //      barrier, no cooperative launch: a block only ever waits on lower-numbered blocks, which the
 //      hardware dispatched before it;

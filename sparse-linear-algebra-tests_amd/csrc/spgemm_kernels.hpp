@@ -2769,13 +2769,14 @@ __device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long l
 // earlier tiles' epoch-tagged status words (an aggregate, or an inclusive prefix that ends the walk)
 // and publish the tile's own inclusive prefix; returns its exclusive prefix. Tiles are taken in
 // ticket (or resident block) order, so every earlier tile belongs to a block that is running or
-// done and never waits on a later one. Lane j reads tile - 1 - j, so one round covers 64
-// predecessors (the nearest inclusive prefix by ballot, the aggregates before it by a wave sum)
-// instead of one dependent load per predecessor. Many small tiles arriving together (k_lane: ~400 one-wave blocks)
-// made the lane-0 walk a chain of hundreds of loads. Called by every lane of the wave; returns the
-// tile's exclusive prefix in every lane.
+// done and never waits on a later one. A round reads kLookR predecessors per lane (the nearest
+// inclusive prefix by ballot, the aggregates before it by a wave sum) instead of one dependent load
+// per predecessor: many small tiles arriving together (k_lane: ~400 one-wave blocks) made a lane-0
+// walk a chain of hundreds of loads. Called by every lane of the wave; returns the tile's exclusive
+// prefix in every lane.
 // (split in two: lookback_publish stores the tile's aggregate (tile 0: its inclusive prefix), and
-// lookback_walk reads the predecessors, so a caller can do work that does not need the offset in between)
+// lookback_walk reads the predecessors, so a caller can do work that does not need the offset in
+// between)
 __device__ __forceinline__ void lookback_publish(unsigned long long *status, uint64_t tile, uint32_t epoch,
                                                  unsigned long long agg) {
     const unsigned long long tag = (unsigned long long)epoch << 42;
@@ -2783,6 +2784,7 @@ __device__ __forceinline__ void lookback_publish(unsigned long long *status, uin
         __hip_atomic_store(&status[tile], tag | (tile == 0 ? kStInc : kStAgg) | agg, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
+constexpr int kLookR = 4;  // predecessors per lane per round of the walk
 __device__ __forceinline__ unsigned long long lookback_walk(unsigned long long *status, uint64_t tile, uint32_t epoch,
                                                             unsigned long long agg) {
     auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -2793,25 +2795,41 @@ __device__ __forceinline__ unsigned long long lookback_walk(unsigned long long *
     const unsigned long long tag = (unsigned long long)epoch << 42;
     if (tile == 0) return 0;
     unsigned long long excl = 0;
-    for (int64_t j0 = (int64_t)tile - 1;; j0 -= kWave) {
-        const int64_t j = j0 - lane;
-        unsigned long long x = 0;
+    // round: lane l reads predecessors tile - 1 - (l * kLookR + i), i < kLookR, so one round covers
+    // 256 (a grid whose blocks arrive together walks back to block 0: k_lane's 422 blocks took 7
+    // rounds of 64, each a device-scope load latency, ~7 us; now 2)
+    for (int64_t j0 = (int64_t)tile - 1;; j0 -= kWave * kLookR) {
+        unsigned long long x[kLookR];
         while (true) {
             bool ok = true;
-            if (j >= 0) {
-                x = ld(&status[j]);
-                ok = (x >> 42) == epoch && (x & (kStAgg | kStInc)) != 0;
-            }
+            sfor<kLookR>([&](auto I) {
+                const int64_t j = j0 - (lane * kLookR + I);
+                x[I] = 0;
+                if (j >= 0) x[I] = ld(&status[j]);
+            });
+            sfor<kLookR>([&](auto I) {
+                const int64_t j = j0 - (lane * kLookR + I);
+                if (j >= 0) ok = ok && (x[I] >> 42) == epoch && (x[I] & (kStAgg | kStInc)) != 0;
+            });
             if (__ballot(!ok) == 0) break;
             __builtin_amdgcn_s_sleep(1);
         }
-        const unsigned long long inc = __ballot(j >= 0 && (x & kStInc));
-        // lanes up to the nearest inclusive prefix (all 64 when there is none in this round)
-        const int last = inc ? (int)__builtin_ctzll(inc) : kWave - 1;
-        unsigned long long v = (j >= 0 && lane <= last) ? (x & kStVal) : 0ull;
+        // the lane's nearest inclusive prefix (kLookR: none), then the wave's nearest by ballot
+        int first = kLookR;
+        sfor<kLookR>([&](auto I) {
+            const int64_t j = j0 - (lane * kLookR + I);
+            if (first == kLookR && j >= 0 && (x[I] & kStInc)) first = I;
+        });
+        const unsigned long long inc = __ballot(first < kLookR);
+        const int last = inc ? (int)__builtin_ctzll(inc) : kWave;  // the lane holding it (kWave: none)
+        unsigned long long v = 0;
+        sfor<kLookR>([&](auto I) {
+            const int64_t j = j0 - (lane * kLookR + I);
+            if (j >= 0 && (lane < last || (lane == last && (int)I <= first))) v += x[I] & kStVal;
+        });
         v = wave_incl_scan_u64(v);
         excl += readlane_u64(v, kWave - 1);
-        if (inc) break;
+        if (inc || j0 - (int64_t)(kWave * kLookR) < 0) break;
     }
     if (lane == 0) st(&status[tile], tag | kStInc | (excl + agg));
     return excl;

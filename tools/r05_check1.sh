@@ -7,6 +7,10 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 $OUT/pytest.log
 timeout -k 10 120 python3 tools/c4_eighth.py > $OUT/c4_eighth.json 2>&1 || { tail $OUT/c4_eighth.json; exit 1; }
 cat $OUT/c4_eighth.json
+SLAT_LIB_PATH=tools/var/libslat_base4.so timeout -k 10 120 python3 tools/c4_eighth.py > $OUT/c4_eighth_base4.json 2>&1 || { tail $OUT/c4_eighth_base4.json; exit 1; }
+cat $OUT/c4_eighth_base4.json
+timeout -k 10 300 python3 tools/ab_heavy.py --big --reps 1 --legs c5ord,c5big_ord,c5any,c5big_any tree base4 > $OUT/heavy.txt 2>&1 || { tail $OUT/heavy.txt; exit 1; }
+tail -6 $OUT/heavy.txt
 SLAT_LIB_PATH=tools/var/libslat_knobs.so SLAT_HOSTIO_CLOCK=1 timeout -k 10 120 python3 tools/e2e_ab.py > $OUT/e2e.jsonl 2> $OUT/e2e.err || exit 1
 cat $OUT/e2e.jsonl; tail -3 $OUT/e2e.err
 timeout -k 10 60 python3 - <<'PY'
