@@ -844,14 +844,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
             const char *e = slat_ab_knob("SLAT_TILE_ROWS");
             return e ? (uint32_t)std::min(64, std::max(8, std::atoi(e))) : 0u;
         }();
-        if (asym.wide) {
-            // tiles of fewer rows when 64-row tiles would leave short-row waves idle: one rank's
-            // eighth of C4 (125 000 rows) took 0.49 ms in 64-row tiles (1953 tiles for ~5 000 waves),
-            // 0.32 / 0.30 / 0.29 in 32 / 16 / 8; the whole C4 (1 M rows) 1.27 ms in 64-row tiles,
-            // 1.29 / 1.30 / 1.35 in smaller ones (profiles/r04_ab12.txt): about 32 tiles per CU
-            const uint64_t t = n / ((uint64_t)ctx->cu_count * 32);
-            a.tile_rows = asym.tile_rows = kTileRows ? kTileRows : (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, t));
-        }
+        if (asym.wide && kTileRows) a.tile_rows = asym.tile_rows = kTileRows;  // (else by occupancy, below)
         if (!asym.wide) {
             a.sym_cap = asym.sym_cap = kHashT / 2;  // every counted row fits numeric's table
             // tiles of fewer rows when 64-row tiles would leave most resident waves idle (27 000 rows:
@@ -887,6 +880,24 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     }();
     const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * kSymBpc)));
     const int sem = dt == SLAT_U32 ? kSemU32 : dt == SLAT_SAT64 ? kSemSat64 : f64any ? kSemF64Any : kSemF64;
+    if (sym_batched && asym.wide && !a.tile_rows) {
+        // Short-row tiles of the wide launches (each a wave's unit of work) sized so the tiles fill
+        // the kernel's resident waves W in whole rounds: T = n / (k W) rows with k = the number of
+        // rounds of ~48-row tiles (8 <= T <= 64). A row block of C4 (one rank's eighth, 125 000
+        // rows) took 0.49 ms in 64-row tiles (1953 tiles for ~5 000 waves) and ~0.30 in 15-row ones:
+        // 8 333 tiles over 5 120 waves is two rounds, the second 60 % full; 25-row tiles are one
+        // round. The whole C4 (1 M rows) keeps ~48-64-row tiles (1.27 ms at 64, 1.35 at 8: a tile's
+        // fixed cost, profiles/r04_ab12.txt)
+        auto rows_for = [&](uint64_t waves) {
+            waves = std::max<uint64_t>(waves, 1);
+            const uint64_t k = std::max<uint64_t>(1, (n + waves * 24) / (waves * 48));
+            return (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, (n + waves * k - 1) / (waves * k)));
+        };
+        const uint64_t cus = (uint64_t)ctx->cu_count;
+        asym.tile_rows = rows_for(cus * wpb * slat_symbolic_short_blocks_per_cu(idx32, ell, (size_t)wpb * sym_short_bytes()));
+        a.tile_rows = batched ? rows_for(cus * wpb * slat_numeric_blocks_per_cu(sem, 3, idx32, ell, hash_lds))
+                              : asym.tile_rows;
+    }
     const int hash_mode = batched ? 3 : 1;  // numeric instance of the short rows of a wide launch
     auto num_grid = [&](int mode, size_t lds) {
         const int nbpc = slat_numeric_blocks_per_cu(sem, mode, idx32, ell, lds);

@@ -36,3 +36,22 @@ hipError_t slat_launch_symbolic_short(bool idx32, bool ell, dim3 grid, size_t ld
     }
     return hipGetLastError();
 }
+
+int slat_symbolic_short_blocks_per_cu(bool idx32, bool ell, size_t lds) {
+    static thread_local int cache_nb[4] = {};
+    static thread_local size_t cache_lds[4] = {};
+    const int ci = (idx32 ? 1 : 0) | (ell ? 2 : 0);
+    if (cache_lds[ci] == lds && cache_nb[ci] > 0) return cache_nb[ci];
+    int nb = 0;
+    hipError_t e;
+    if (idx32)
+        e = ell ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_symbolic_short<uint32_t, false>, kBlock, lds)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_symbolic_short<uint32_t, true>, kBlock, lds);
+    else
+        e = ell ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_symbolic_short<uint64_t, false>, kBlock, lds)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_symbolic_short<uint64_t, true>, kBlock, lds);
+    nb = (e == hipSuccess && nb > 0) ? nb : 1;
+    cache_lds[ci] = lds;
+    cache_nb[ci] = nb;
+    return nb;
+}
