@@ -141,6 +141,21 @@ def e2e_leg(ctx, P, A, steps: int):
         fn()  # warm-up (and the pinned pool)
         el = timed_steps(fn, steps, 1, ctx.sync)
         out[name] = (el / steps * 1e3, nnz[0] * steps / el / 1e9)
+    # the same pageable call in a process whose malloc keeps freed arrays in its heap (glibc's
+    # mmap_max = 0; jemalloc / mimalloc, common Rust allocators, do so by default): each call's fresh
+    # output arrays then reuse the previous call's pages instead of a new mmap whose first touch and
+    # munmap cost this VM ~7 ms per 47 MB array each (profiles/r05_e2e_os_costs.txt). A child process,
+    # since the tunable is read at process start
+    import subprocess
+    env = dict(os.environ, GLIBC_TUNABLES="glibc.malloc.mmap_max=0:glibc.malloc.trim_threshold=4294967295")
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "e2e_ab.py"), "--quick", "--mean", str(steps)],
+                           env=env, capture_output=True, text=True, timeout=300)
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+        ms = json.loads(line)["e2e_mean_ms"]
+        out["pageable_heap"] = (ms, nnz[0] / (ms * 1e-3) / 1e9)
+    except Exception:
+        out["pageable_heap"] = None
     return out
 
 
@@ -458,7 +473,10 @@ def emit(args, world, side, power, n, nnz_a, nnz_b, nnz_c, value, ms_per_step, s
                    # host-resident calls (PCIe both ways: the drop-in's cost for Vec in / Vec out)
                    **({"e2e_ms": round(e2e["pageable"][0], 4), "e2e_gnnz_per_s": round(e2e["pageable"][1], 4),
                        "e2e_pinned_ms": round(e2e["pinned"][0], 4),
-                       "e2e_pinned_gnnz_per_s": round(e2e["pinned"][1], 4)} if e2e else {})},
+                       "e2e_pinned_gnnz_per_s": round(e2e["pinned"][1], 4),
+                       **({"e2e_heap_ms": round(e2e["pageable_heap"][0], 4),
+                           "e2e_heap_gnnz_per_s": round(e2e["pageable_heap"][1], 4)} if e2e.get("pageable_heap") else {})}
+                      if e2e else {})},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

@@ -881,17 +881,15 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     const dim3 sym_grid((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * kSymBpc)));
     const int sem = dt == SLAT_U32 ? kSemU32 : dt == SLAT_SAT64 ? kSemSat64 : f64any ? kSemF64Any : kSemF64;
     if (sym_batched && asym.wide && !a.tile_rows) {
-        // Short-row tiles of the wide launches (each a wave's unit of work) sized so the tiles fill
-        // the kernel's resident waves W in whole rounds: T = n / (k W) rows with k = the number of
-        // rounds of ~48-row tiles (8 <= T <= 64). A row block of C4 (one rank's eighth, 125 000
-        // rows) took 0.49 ms in 64-row tiles (1953 tiles for ~5 000 waves) and ~0.30 in 15-row ones:
-        // 8 333 tiles over 5 120 waves is two rounds, the second 60 % full; 25-row tiles are one
-        // round. The whole C4 (1 M rows) keeps ~48-64-row tiles (1.27 ms at 64, 1.35 at 8: a tile's
-        // fixed cost, profiles/r04_ab12.txt)
+        // Short-row tiles of the wide launches (a wave's unit of work): about three tiles per resident
+        // wave W of the kernel, T = n / 3W rows (8 <= T <= 64). Small launches need the rounds: one
+        // rank's eighth of C4 (125 000 rows, W ~ 5 000) took 0.216 ms in 8-row tiles, 0.249 in 24-row
+        // ones (one round: every wave in the same phase at once) and 0.43 in 64-row ones; the whole
+        // C4 (1 M rows) is fastest in 64-row tiles (1.226 ms; 1.315 in 8-row ones: a tile's fixed
+        // cost) (profiles/r05_c4_tile_sweep.txt)
         auto rows_for = [&](uint64_t waves) {
             waves = std::max<uint64_t>(waves, 1);
-            const uint64_t k = std::max<uint64_t>(1, (n + waves * 24) / (waves * 48));
-            return (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, (n + waves * k - 1) / (waves * k)));
+            return (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(8, (n + 3 * waves - 1) / (3 * waves)));
         };
         const uint64_t cus = (uint64_t)ctx->cu_count;
         asym.tile_rows = rows_for(cus * wpb * slat_symbolic_short_blocks_per_cu(idx32, ell, (size_t)wpb * sym_short_bytes()));
@@ -922,7 +920,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
                  o_eval = o_ecol + ecol_b, o_eng = o_eval + eval_b, o_sbm = o_eng + eng_b, o_smask = o_sbm + sbm_b;
     // batched wide launches: symbolic / numeric window-row lists u32[n] | their counters
     const size_t list_b = sym_batched ? up256(n * 4) : 0;
-    const size_t o_l1 = o_smask + smask_b, o_l2 = o_l1 + list_b, o_lc = o_l2 + list_b, lc_b = sym_batched ? 256 : 0;
+    const size_t o_l1 = o_smask + smask_b, o_l2 = o_l1 + list_b, o_lc = o_l2 + list_b, lc_b = 0;
     // fat rows (MAGNUS's dense-accumulation category) once a row can reach slat_fat_min() products:
     // max row of A x max row of B (A's max row unknown: when B has long rows)
     static const bool kNoFat = slat_ab_knob("SLAT_NO_FAT") != nullptr;
@@ -983,7 +981,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         else
             be = launch_build_ell<double>(s, B, a.ell_wq, (uint32_t *)a.ell_col, (void *)a.ell_val, (uint8_t *)a.ell_ng, nullptr);
         SLAT_HIP(ctx, be);
-    } else if (a.b_vmax && B->nnz) {
+    } else if (a.b_vmax && B->nnz && !pell) {
         const unsigned g = (unsigned)std::min<uint64_t>((B->nnz + kBlock - 1) / kBlock, (uint64_t)ctx->cu_count * 4);
         if (dt == SLAT_U32)
             hipLaunchKernelGGL(k_bvmax<uint32_t>, dim3(g), dim3(kBlock), 0, s, (const uint32_t *)B->values, B->nnz,
@@ -1141,10 +1139,12 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     if (sym_batched) {
         // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
         // row's products per tile, listing the rest), then the listed rows by windows
-        // (every row short: no lists, so no counters to clear)
-        unsigned int *lc = all_short ? nullptr : (unsigned int *)(ws + o_lc);
-        if (lc) SLAT_HIPC(hipMemsetAsync(lc, 0, lc_b, s));
+        // the lists' lengths: epoch-tagged words of the context (d_words[8] symbolic, [10] numeric),
+        // no clear per call
+        unsigned long long *lc = all_short ? nullptr : ctx->d_words + 8;
+        const uint32_t lep = ++ctx->list_epoch ? ctx->list_epoch : ++ctx->list_epoch;  // (0 never: a zeroed word)
         Args h1 = asym, h2 = asym;
+        h1.list_epoch = h2.list_epoch = a.list_epoch = lep;
         h1.cbits = a.cbits;
         h1.list = h2.list = all_short ? nullptr : (uint32_t *)(ws + o_l1);
         h1.list_cnt = h2.list_cnt = lc;
@@ -1158,7 +1158,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
             SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
         }
         a.list = all_short ? nullptr : (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
-        a.list_cnt = all_short ? nullptr : lc + 16;
+        a.list_cnt = all_short ? nullptr : lc + 2;
     } else if (hash) {
         Args h1 = asym;
         h1.tq = (kDyn & 2u) ? tq : nullptr;

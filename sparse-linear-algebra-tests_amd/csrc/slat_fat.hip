@@ -567,45 +567,7 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                     }
                 });
             };
-            // (the group of kFD entries when every one has at most one product in this slice, the
-            // common case: ~0.4 products per entry and slice on C5) each entry's product moves to lane
-            // U; when the group's columns are distinct the lanes add in parallel, one LDS round trip
-            // for the group instead of one per entry (same sums: one product per column per group, and
-            // the groups stay in A order). A repeated column takes the per-entry path below.
-            auto apply_single = [&](const Ent &q) -> bool {
-                bool single = true;
-                sfor<kFD>([&](auto U) { single = single && q.e[U] - q.s[U] <= (I)1; });
-                if (!single) return false;  // wave-uniform
-                uint32_t c = kSent;
-                S pr = S(0);
-                sfor<kFD>([&](auto U) {
-                    if (q.s[U] != q.e[U]) {  // wave-uniform
-                        const uint32_t cu = readlane_u32(q.c[U], 0);
-                        const S vu = readlane_val(q.v[U], 0);
-                        if (lane == (int)U) {
-                            c = cu;
-                            pr = __dmul_rn(q.a[U], vu);
-                        }
-                    }
-                });
-                // a repeated column among the group's lanes (16-lane rotations)
-                bool dup = false;
-                sfor<kFD - 1>([&](auto D) {
-                    const int src = (lane & ~(kFD - 1)) | ((lane + (int)D + 1) & (kFD - 1));
-                    const uint32_t o = (uint32_t)__shfl((int)c, src);
-                    dup = dup || (c != kSent && o == c);
-                });
-                if (__ballot(dup)) return false;
-                if (c != kSent) {
-                    const uint32_t o = c - c0;
-                    acc[o] = __dadd_rn(acc[o], pr);
-                    atomicOr(&bits[o >> 5], 1u << (o & 31));
-                }
-                wave_sync();
-                return true;
-            };
             auto apply = [&](const Ent &q) {
-                if (kFD <= kWave && apply_single(q)) return;
                 sfor<kFD>([&](auto U) {
                     const I s = q.s[U], e = q.e[U];
                     if (s != e) {  // wave-uniform

@@ -44,10 +44,12 @@ struct slat_ctx {
     unsigned long long done_seq = 0;         // last sequence number queued to [7]
     unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word,
                                              // [4] check flags, [5] work tickets (zeroed by each launch's last taker),
-                                             // [6] unused,
+                                             // [6] unused, [8] / [10] the short-row kernels' list lengths
+                                             // (tagged list_epoch),
     unsigned long long *d_done = nullptr;    // the call's last kernel's two-level done count (signal_done)
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
+    uint32_t list_epoch = 0;                 // per-call tag of the list lengths d_words[8] / [10]
     // (A, B, row block) triples whose lane-kernel attempt overflowed (a row past slat_lane_cap()
     // products): the next call on the same triple goes to the pipeline directly instead of running
     // both. Keyed by both operands' arrays, sizes and the row range; an entry whose array the context

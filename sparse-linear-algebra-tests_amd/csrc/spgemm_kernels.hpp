@@ -126,7 +126,10 @@ struct Args {
     // rows of the window category, appended by the short-row kernels (symbolic / numeric lists)
     // and walked by the MODE 2 launches instead of every row
     uint32_t *list;
-    unsigned int *list_cnt;  // max row length of B (the symbolic pass's product bound: len(A row) * b_maxrow)
+    // the list's length, epoch-tagged ((list_epoch << 32) | count; another tag reads as 0), so no
+    // per-call clear (a memset launch: 4.8 us of a C4 row block's ~220)
+    unsigned long long *list_cnt;
+    uint32_t list_epoch;
     unsigned long long *host_out;  // mapped pinned host words: [0] nnz, [1] max row nnz, [2] rows with zeros
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
@@ -160,6 +163,12 @@ struct Args {
 };
 
 __device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.fr_mark && p.fr_mark[row]; }
+
+// the length of the window-category list the short-row kernels appended to (their launch's tag)
+__device__ __forceinline__ uint64_t list_len(const Args &p) {
+    const unsigned long long w = __hip_atomic_load(p.list_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (uint64_t)__builtin_amdgcn_readfirstlane((w >> 32) == p.list_epoch ? (uint32_t)w : 0u);
+}
 
 // End of the call's last kernel (p.seq != 0): the last block to finish stores seq into the mapped host
 // word the host spins on (host_out[7]), in place of a one-thread kernel queued behind this one (a
@@ -1617,7 +1626,7 @@ void k_symbolic(Args p) {
         __syncthreads();
     }
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
-    const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
+    const uint64_t nit = listed ? list_len(p) : p.nrows;
     // a wave with no listed row leaves before touching LDS (C4 lists none: the launch is then
     // only its dispatch)
     if (listed && !p.bmax && (uint64_t)blockIdx.x * kWpb + wv >= nit) return;
@@ -1687,7 +1696,7 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
 
     const int lane = lane_id();
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_numeric_short
-    const uint64_t nit = listed ? (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt) : p.nrows;
+    const uint64_t nit = listed ? list_len(p) : p.nrows;
     // a wave with no listed row leaves before touching LDS (C4 lists none)
     if (listed && first >= nit) return;
     const NumLayout lay = num_layout(p.ww, p.area);
@@ -2097,7 +2106,16 @@ __device__ __forceinline__ void list_rows(const Args &p, bool take, uint64_t r) 
     const unsigned long long m = __ballot(take);
     if (!m) return;
     unsigned int base = 0;
-    if (lane_id() == 0) base = atomicAdd(p.list_cnt, (unsigned int)__popcll(m));
+    if (lane_id() == 0) {
+        // (tagged counter: a word of another call's tag counts from 0)
+        const unsigned long long tag = (unsigned long long)p.list_epoch << 32;
+        unsigned long long old = __hip_atomic_load(p.list_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nv;
+        do {
+            base = (old & ~0xFFFFFFFFull) == tag ? (unsigned int)old : 0u;
+            nv = tag | (base + (unsigned int)__popcll(m));
+        } while (!__hip_atomic_compare_exchange_strong(p.list_cnt, &old, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+    }
     base = __builtin_amdgcn_readfirstlane(base);
     if (take) p.list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)r;
 }

@@ -31,7 +31,7 @@ def main():
     A = slat.torus_thinned_device(100, 3.0, slat.StdRng(), ctx)
     P = A.matmul(A).matmul(A)
     n = P.n
-    B = A.prepare()
+    B = A.prepare() if hasattr(slat.lib(), "slat_bprep_create") else A  # (an older library: per-call image)
     for _ in range(3):
         P.matmul_rowblock(0, n, B)
     full = timed(lambda: P.matmul_rowblock(0, n, B))

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """The drop-in's host-resident call on the headline step (C = A^6 * A, 30^3 torus, u32): H2D of both
 operands, the product, D2H of C into fresh pageable numpy arrays (np.empty per call, as a Rust Vec),
-plus the two copies alone. One JSON line; run once per library (SLAT_LIB_PATH) / knob setting."""
+plus the two copies alone. One JSON line; run once per library (SLAT_LIB_PATH) / knob setting.
+--mean K: the mean over K calls after one warm-up (bench.py's e2e timing) as e2e_mean_ms too."""
 import json
 import os
 import sys
@@ -26,6 +27,11 @@ def med(fn, n=10):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mean", type=int, default=0)
+    ap.add_argument("--quick", action="store_true", help="the end-to-end call only")
+    args = ap.parse_args()
     ctx = slat.default_context(0)
     A = slat.CsrMatrix.from_host(slat.torus_thinned(30, 3.0, slat.StdRng()), ctx)
     P = A
@@ -43,6 +49,18 @@ def main():
         nnz[0] = slat.spgemm_host(hP, hA, ctx).nnz
 
     out["e2e_ms"] = med(e2e)
+    if args.mean:
+        e2e()
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.mean):
+            e2e()
+        ctx.sync()
+        out["e2e_mean_ms"] = round((time.perf_counter() - t0) / args.mean * 1e3, 4)
+    if args.quick:
+        out["nnz"] = nnz[0]
+        print(json.dumps(out), flush=True)
+        return
     out["h2d_P_ms"] = med(lambda: slat.CsrMatrix.from_host(hP, ctx))
 
     def d2h():
