@@ -842,7 +842,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         a.cbits = cb <= 25 ? cb : 0;
         static const uint32_t kTileRows = [] {  // A/B knob: rows per tile (8 .. 64)
             const char *e = slat_ab_knob("SLAT_TILE_ROWS");
-            return e ? (uint32_t)std::min(64, std::max(8, std::atoi(e))) : 0u;
+            return e ? (uint32_t)std::min(64, std::max(2, std::atoi(e))) : 0u;
         }();
         if (asym.wide && kTileRows) a.tile_rows = asym.tile_rows = kTileRows;  // (else by occupancy, below)
         if (!asym.wide) {
