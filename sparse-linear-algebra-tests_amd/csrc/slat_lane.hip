@@ -1,29 +1,35 @@
 // slat_lane.hip — products whose rows are all short (at most kLaneCap products each: the 30^3 chain's
-// C1 = A * A, 27 000 rows of ~12 products) in ONE kernel, a row per LANE (SURVEY.md §8(d) config C1;
-// the fixed per-row cost of the single-window path).
+// C1 = A * A, 27 000 rows of ~12 products) in ONE kernel (VERDICT round 3
+// item 3, round 4 item 4).
 //
 // The pipeline gives such a call four launches and a wave per row, so each wave walks ~9 rows of ~12
 // products one after another, every row a chain of dependent loads (bounds, A entries, B rows, stored
-// bitmap) that nothing hides: C1 took 88 us, 46 of them in k_numeric. Here a wave owns 64 rows:
+// bitmap) that nothing hides: C1 took 88 us, 46 of them in k_numeric. Here a block of four waves
+// owns 64 consecutive rows, 16 per wave:
 //
-//   1. the rows' A entries (contiguous in A) are walked 256 at a time, four per lane; each entry
+//   1. a wave's rows' A entries (contiguous in A) are walked 64 at a time, one per lane; each entry
 //      learns its row (a marker at the row's first entry, a running max), its B row's length, and its
 //      products' offset in the wave's flattened product space (a wave prefix);
-//   2. the products are walked flattened, 256 per pass, every lane on one (an entry by markers, as
-//      the fat rows' fr_flat) and written into their row's lane of an LDS slot table (slot s of row l
-//      at s * rows + l) as (column << 6 | slot, product): the slot is the product's position in the
+//   2. the products are walked flattened, 64 per round, every lane on one (an entry by markers, as
+//      the fat rows' fr_flat) and written into their row's column of an LDS slot table (slot s of row
+//      r at s * 16 + r) as (column << 6 | slot, product): the slot is the product's position in the
 //      row, A order then B order, so the key is unique and keeps the reference's order for equal
 //      columns;
-//   3. every lane sorts its row's keys in registers (a bitonic network of 16, 32 or 64 keys, the
-//      wave's longest row decides; the values stay in LDS, found by the slot in the key) and counts
-//      its distinct columns;
-//   4. the wave's offset by a decoupled look-back over the earlier waves' status words (one wave per
-//      block; lookback_walk reads 256 predecessors per round), then row_ptr, and the rows'
-//      sums in key order — the f64 left fold from 0.0 in A order, the saturating integer sums — are
-//      stored; zero sums (explicit zero inputs, f64 cancellation) are counted for the host's
-//      compaction, as after k_numeric. The last block stores
-//      nnz, the max row and the completion word.
+//   3. each row's keys are sorted by its QUAD of lanes (a bitonic network of 16, 32 or 64 keys, the
+//      wave's longest row decides, 4 / 8 / 16 per lane, DPP quad permutes across the quad) and
+//      written back row-major; the quad's first lane then holds the row's sorted keys and counts its
+//      distinct columns;
+//   4. the block's offset by a decoupled look-back over the earlier blocks' status words (the block
+//      aggregate published first, lookback_walk reads 256 predecessors per round); meanwhile u32
+//      rows sum equal columns in key order — the saturating integer sums, the f64 left fold from 0.0
+//      in A order — into an LDS staging area at their block-local offsets, which the block stores
+//      coalesced once its offset is known (8-byte values are summed and stored after the
+//      look-back); zero sums (explicit zero inputs, f64 cancellation) are counted for the host's
+//      compaction, as after k_numeric. The last block stores nnz, the max row and the completion
+//      word.
 //
+// Round 4's version gave each row one LANE (a 64-key network per lane, 64 rows per one-wave block):
+// 422 waves for C1 on 1 024 SIMDs, each a long chain; here four times the waves share it.
 // A row of more than kLaneCap products sets the mapped overflow word: the host then runs the call
 // through the pipeline (the host only tries this kernel when max row(A) x max row(B) <= 4 kLaneCap).
 #include <hip/hip_runtime.h>
@@ -37,23 +43,30 @@ using namespace slat;
 
 namespace {
 
-constexpr uint32_t kLaneCap = 64;   // products per row (sort slots per lane)
-constexpr uint32_t kLaneRows = 64;  // rows per one-wave block (a row per lane)
-constexpr uint32_t kLaneSeg = 256;  // A entries / products per pass (four per lane)
+constexpr uint32_t kLaneCap = 64;                     // products per row (sort slots per row)
+constexpr uint32_t kQR = 16;                          // rows per wave (a quad of lanes per row)
+constexpr uint32_t kLaneWaves = 4;                    // waves per block
+constexpr uint32_t kLaneRows = kQR * kLaneWaves;      // rows per block
+constexpr uint32_t kLaneSeg = kWave;                  // A entries per pass (one per lane)
 #ifndef SLAT_LANE_PG
 #define SLAT_LANE_PG 4
 #endif
-constexpr uint32_t kLanePG = SLAT_LANE_PG;  // product passes whose loads are issued together (variant builds: 1)
+constexpr uint32_t kLanePG = SLAT_LANE_PG;  // product passes of 64 whose loads are issued together
 
+// LDS of one wave: slot keys u32[64 * 16] (slot-major, then the sorted keys row-major) | slot values
+// S[64 * 16] | entry bases u32[64] | entry A values S[64] | entry rows u8[64] | entry markers u8[64] |
+// product markers u16[64 * PG] | row bases u32[16] | row counts u32[16]
+template <typename S>
+__host__ __device__ constexpr size_t lane_wave_lds() {
+    return ((size_t)kLaneCap * kQR * (4 + sizeof(S)) + kLaneSeg * (4 + sizeof(S) + 1 + 1) + kLaneSeg * kLanePG * 2 +
+            kQR * 8 + 15) & ~(size_t)15;
+}
+// the block: four wave regions | (u32 values) the block's outputs staged, columns u32[64 * 64] and
+// values u32[64 * 64], so they are stored coalesced once the block's offset is known | wave sums
+// u32[4] | the block's max row u32 | the broadcast offset u64
 template <typename S>
 __host__ __device__ constexpr size_t lane_lds() {
-    // slot keys u32[64 * rows] | slot values S[64 * rows] | entry bases u32[256] | entry A values S[256] |
-    // entry rows u8[256] | entry markers u8[256] | product markers u16[256] | row bases u32[64] |
-    // row counts u32[64]
-    // (+ u32 values: an output-value staging area u32[64 * rows], so the wave's outputs are stored
-    // coalesced; the columns stage in the slot keys' area, free once the keys are in registers)
-    return (size_t)kLaneCap * kLaneRows * (4 + sizeof(S)) + kLaneSeg * (4 + sizeof(S) + 1 + 1 + 2 * kLanePG) + kWave * 8 +
-           (sizeof(S) == 4 ? (size_t)kLaneCap * kLaneRows * 4 : 0);
+    return lane_wave_lds<S>() * kLaneWaves + (sizeof(S) == 4 ? (size_t)kLaneCap * kLaneRows * 8 : 0) + 32;
 }
 
 // the semiring's running sum of one output
@@ -83,39 +96,48 @@ struct LaneSum {
     }
 };
 
-// ascending bitonic sort of the lane's N keys (compile-time indices only). The keys are unique
-// (column << 6 | slot) and carry their slot, so no payload moves: each compare-exchange is one min
-// and one max
-template <int N>
-__device__ __forceinline__ void lane_sort(uint32_t (&k)[kLaneCap]) {
+// Ascending bitonic sort of a row's N keys held by its quad of lanes, NL = N / 4 per lane (element
+// e = q * NL + j of lane q's register j). The keys are unique (column << 6 | slot) and carry their
+// slot, so no payload moves: a compare-exchange is a min and a max. Strides below NL stay in a lane;
+// NL and 2 NL exchange with lane q ^ 1 / q ^ 2 of the quad (DPP quad permutes). Against one lane
+// per row (a 64-key network per lane, 672 compare-exchanges on C1) the row's sort is ~2.5x shorter
+// and a wave holds 16 rows, not 64, so four times the waves share the work.
+template <int NL>
+__device__ __forceinline__ void quad_sort(uint32_t (&k)[kLaneCap / 4], uint32_t q) {
+    constexpr int N = 4 * NL;
 #pragma unroll
-    for (int size = 2; size <= N; size <<= 1)
+    for (int size = 2; size <= N; size <<= 1) {
 #pragma unroll
-        for (int stride = size / 2; stride > 0; stride >>= 1)
+        for (int stride = size / 2; stride > 0; stride >>= 1) {
+            if (stride < NL) {
 #pragma unroll
-            for (int i = 0; i < N; ++i) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const uint32_t lo = min(k[i], k[j]), hi = max(k[i], k[j]);
-                    const bool asc = (i & size) == 0;
-                    k[i] = asc ? lo : hi;
-                    k[j] = asc ? hi : lo;
+                for (int j = 0; j < NL; ++j) {
+                    const int pj = j ^ stride;
+                    if (pj > j) {
+                        // ascending iff element e = q * NL + j has bit `size` clear
+                        const bool asc = size >= N ? true : size < NL ? (j & size) == 0 : ((q * NL) & size) == 0;
+                        const uint32_t lo = min(k[j], k[pj]), hi = max(k[j], k[pj]);
+                        k[j] = asc ? lo : hi;
+                        k[pj] = asc ? hi : lo;
+                    }
+                }
+            } else {
+                const uint32_t m = (uint32_t)(stride / NL);  // 1 or 2: the partner lane q ^ m
+                const bool lower = (q & m) == 0;
+                const bool asc = size >= N ? true : ((q * NL) & size) == 0;
+                const bool keep_min = lower == asc;
+#pragma unroll
+                for (int j = 0; j < NL; ++j) {
+                    const uint32_t o = m == 1 ? lane_xor<1>(k[j]) : lane_xor<2>(k[j]);
+                    k[j] = keep_min ? min(k[j], o) : max(k[j], o);
                 }
             }
+        }
+    }
 }
 
-// the lane's sorted keys: distinct columns (the row's structural count; no values read)
-template <int N>
-__device__ __forceinline__ uint32_t lane_count(const uint32_t (&k)[kLaneCap]) {
-    uint32_t nz = 0;
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-        nz += (k[i] != kSent && (i == 0 || (k[i] >> 6) != (k[i - 1] >> 6))) ? 1u : 0u;
-    return nz;
-}
-
-// the lane's sorted keys: emit(col, value, index) for each column's sum in column order (values by
-// slot from the lane's column of the slot table); returns the number of zero sums among them
+// the row's sorted keys (all N in one lane): emit(col, value, index) for each column's sum in column
+// order (values by slot: the row's column of the slot table, stride kQR); returns the zero sums
 template <typename Sem, int N, typename F>
 __device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], const typename Sem::S *sv, F &&emit) {
     using L = LaneSum<Sem>;
@@ -124,7 +146,7 @@ __device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], 
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const uint32_t c = k[i] == kSent ? kSent : k[i] >> 6;
-        const typename Sem::S v = c == kSent ? typename Sem::S(0) : sv[(k[i] & 63u) * kLaneRows];
+        const typename Sem::S v = c == kSent ? typename Sem::S(0) : sv[(k[i] & 63u) * kQR];
         if (c != prev) {
             if (prev != kSent) {
                 const auto out = L::done(s);
@@ -146,113 +168,101 @@ __device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], 
 }
 
 template <typename Sem>
-__global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *status, uint32_t epoch,
-                                                unsigned long long *maxw) {
+__global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned long long *status, uint32_t epoch,
+                                                               unsigned long long *maxw) {
     using S = typename Sem::S;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t *skey = (uint32_t *)smem;
-    S *sval = (S *)(smem + kLaneCap * kLaneRows * 4);
-    uint8_t *q = smem + kLaneCap * kLaneRows * (4 + sizeof(S));
-    uint32_t *eb = (uint32_t *)q;
-    S *ea = (S *)(q + kLaneSeg * 4);
-    uint8_t *erl = q + kLaneSeg * (4 + sizeof(S));
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    uint8_t *wr = smem + (size_t)wv * lane_wave_lds<S>();
+    uint32_t *skey = (uint32_t *)wr;
+    S *sval = (S *)(wr + kLaneCap * kQR * 4);
+    uint8_t *q8 = wr + kLaneCap * kQR * (4 + sizeof(S));
+    uint32_t *eb = (uint32_t *)q8;
+    S *ea = (S *)(q8 + kLaneSeg * 4);
+    uint8_t *erl = q8 + kLaneSeg * (4 + sizeof(S));
     uint8_t *amk = erl + kLaneSeg;
     uint16_t *pmk = (uint16_t *)(amk + kLaneSeg);
-    uint32_t *rbase = (uint32_t *)(pmk + kLaneSeg * kLanePG), *rcnt = rbase + kWave;
-    S *stg = (S *)(rcnt + kWave);  // (u32 values) the outputs' value staging
-    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t *rbase = (uint32_t *)(pmk + kLaneSeg * kLanePG), *rcnt = rbase + kQR;
+    uint8_t *blk = smem + lane_wave_lds<S>() * kLaneWaves;
+    uint32_t *stc = (uint32_t *)blk;                          // (u32 values) staged columns
+    S *stv = (S *)(blk + (size_t)kLaneCap * kLaneRows * 4);   // (u32 values) staged values
+    uint32_t *s_wsum = (uint32_t *)(blk + (sizeof(S) == 4 ? (size_t)kLaneCap * kLaneRows * 8 : 0));
+    uint32_t *s_max = s_wsum + kLaneWaves;
+    unsigned long long *s_off = (unsigned long long *)(s_max + 4);
     const S *av = (const S *)p.a_val;
     const S *bv = (const S *)p.b_val;
     const auto plus = [](uint32_t x, uint32_t y) { return x + y; };
     const auto mx = [](uint32_t x, uint32_t y) { return max(x, y); };
 
-    PhaseClock pc{};  // diagnostic builds (SLAT_PHASES): where a wave's time goes
-    if constexpr (SLAT_PHASES) pc.t = __builtin_amdgcn_s_memtime();
-    const uint64_t r0 = (uint64_t)blockIdx.x * kLaneRows, r = r0 + lane;
-    const uint32_t nt = (uint32_t)min<uint64_t>(kLaneRows, p.nrows - r0);
+    // this wave's rows [r0, r0 + nt): lanes < nt hold their bounds
+    const uint64_t r0 = (uint64_t)blockIdx.x * kLaneRows + (uint64_t)wv * kQR;
+    const uint32_t nt = r0 < p.nrows ? (uint32_t)min<uint64_t>(kQR, p.nrows - r0) : 0u;
     uint32_t A0j = 0, A1j = 0;
     if (lane < nt) {
-        A0j = (uint32_t)p.a_rp[r];
-        A1j = (uint32_t)p.a_rp[r + 1];
+        A0j = (uint32_t)p.a_rp[r0 + lane];
+        A1j = (uint32_t)p.a_rp[r0 + lane + 1];
     }
-    const uint32_t A0 = readlane_u32(A0j, 0), A1 = readlane_u32(A1j, (int)nt - 1);
-    for (uint32_t w = lane; w < kLaneSeg / 4; w += kWave) ((uint32_t *)amk)[w] = 0;
+    const uint32_t A0 = nt ? readlane_u32(A0j, 0) : 0u, A1 = nt ? readlane_u32(A1j, (int)nt - 1) : 0u;
+    amk[lane] = 0;
     for (uint32_t w = lane; w < kLaneSeg * kLanePG / 2; w += kWave) ((uint32_t *)pmk)[w] = 0;
-    rcnt[lane] = 0;
-    rbase[lane] = 0;
-    wave_sync();
+    if (lane < kQR) {
+        rcnt[lane] = 0;
+        rbase[lane] = 0;
+    }
+    if (threadIdx.x == 0) *s_max = 0;
+    __syncthreads();  // (the block's max row word is clear before any wave adds to it)
 
-    pc.mark(0);  // row bounds, LDS init
-    // 1-2. entries 256 at a time, then their products flattened
-    uint32_t rcarry = 0, fcarry = 0;  // row lane (+1) running into the segment, flat products so far
+    // 1-2. the rows' entries 64 at a time, then their products flattened into the slot table
+    uint32_t rcarry = 0, fcarry = 0;  // row (+1) running into the pass, flat products so far
     for (uint32_t sb = A0; sb < A1; sb += kLaneSeg) {
-        // each row's first entry in this segment marks its lane (a later non-empty row wins a tie
-        // with empty rows before it)
+        // each row's first entry in this pass marks its row (a later non-empty row wins a tie with
+        // empty rows before it)
         if (lane < nt && A1j > A0j && A0j >= sb && A0j - sb < kLaneSeg) amk[A0j - sb] = (uint8_t)(lane + 1);
         wave_sync();
-        uint32_t rl[4], kq[4], bl[4], off[4], first[4];
-        S aq[4];
-        sfor<4>([&](auto Q) {
-            const uint32_t i = sb + Q * kWave + lane;
-            const uint32_t m = amk[Q * kWave + lane];
-            first[Q] = m;
-            const uint32_t run = max(wave_incl_scan(m, 0u, mx), rcarry);
-            rcarry = readlane_u32(run, kWave - 1);
-            rl[Q] = run - 1;
-            kq[Q] = kSent;
-            aq[Q] = S(0);
-            if (i < A1) {
-                kq[Q] = p.a_col[i];
-                aq[Q] = av[i];
-            }
-        });
-        sfor<4>([&](auto Q) { amk[Q * kWave + lane] = 0; });
-        uint32_t bs[4];
-        sfor<4>([&](auto Q) {
-            bs[Q] = 0;
-            bl[Q] = 0;
-            if (kq[Q] < p.b_nrows) {
-                const uint64_t b0 = p.b_rp[kq[Q]], b1 = p.b_rp[kq[Q] + 1];
-                bs[Q] = (uint32_t)b0;
-                bl[Q] = (uint32_t)min<uint64_t>(b1 - b0, kLaneCap + 1);  // (a longer row overflows)
-            }
-        });
-        uint32_t stot = 0;
-        sfor<4>([&](auto Q) {
-            const uint32_t incl = wave_incl_scan(bl[Q], 0u, plus);
-            off[Q] = fcarry + stot + incl - bl[Q];
-            stot += readlane_u32(incl, kWave - 1);
-        });
-        sfor<4>([&](auto Q) {
-            const uint32_t e = Q * kWave + lane;
-            if (first[Q] && sb + e < A1) rbase[rl[Q]] = off[Q];  // the row's first entry
-            if (sb + e < A1 && bl[Q]) atomicAdd(&rcnt[rl[Q]], bl[Q]);
-            eb[e] = bs[Q] - off[Q];  // product t of the entry: B index eb + t
-            ea[e] = aq[Q];
-            erl[e] = (uint8_t)rl[Q];
-        });
+        const uint32_t i = sb + lane;
+        const uint32_t first = amk[lane];
+        const uint32_t run = max(wave_incl_scan(first, 0u, mx), rcarry);
+        rcarry = readlane_u32(run, kWave - 1);
+        const uint32_t rl = run - 1;
+        uint32_t kq = kSent;
+        S aq = S(0);
+        if (i < A1) {
+            kq = p.a_col[i];
+            aq = av[i];
+        }
+        amk[lane] = 0;
+        uint32_t bs = 0, bl = 0;
+        if (kq < p.b_nrows) {
+            const uint64_t b0 = p.b_rp[kq], b1 = p.b_rp[kq + 1];
+            bs = (uint32_t)b0;
+            bl = (uint32_t)min<uint64_t>(b1 - b0, kLaneCap + 1);  // (a longer row overflows)
+        }
+        const uint32_t incl = wave_incl_scan(bl, 0u, plus);
+        const uint32_t off = fcarry + incl - bl, stot = readlane_u32(incl, kWave - 1);
+        if (first && i < A1) rbase[rl] = off;  // the row's first entry
+        if (i < A1 && bl) atomicAdd(&rcnt[rl], bl);
+        eb[lane] = bs - off;  // product t of the entry: B index eb + t
+        ea[lane] = aq;
+        erl[lane] = (uint8_t)rl;
         wave_sync();
-        pc.mark(1);  // entries: rows, B row bounds, offsets
-        // the segment's products, 256 per pass, kLanePG passes at a time (their loads in flight
+        // the pass's products, 64 per round, kLanePG rounds at a time (their loads in flight
         // together): entry by markers, slot = t - the row's base
-        constexpr uint32_t kSpan = kLaneSeg * kLanePG, kQ = 4 * kLanePG;
+        constexpr uint32_t kSpan = kLaneSeg * kLanePG;
         for (uint32_t p0 = 0; p0 < stot; p0 += kSpan) {
             const uint32_t t0 = fcarry + p0;
-            sfor<4>([&](auto Q) {
-                if (bl[Q] && off[Q] < t0 + kSpan && off[Q] + bl[Q] > t0)
-                    pmk[max(off[Q], t0) - t0] = (uint16_t)(Q * kWave + lane + 1);
-            });
+            if (bl && off < t0 + kSpan && off + bl > t0) pmk[max(off, t0) - t0] = (uint16_t)(lane + 1);
             wave_sync();
-            uint32_t L[kQ], carry = 0;
-            sfor<kQ>([&](auto Q) {
+            uint32_t L[kLanePG], carry = 0;
+            sfor<kLanePG>([&](auto Q) {
                 const uint32_t m = pmk[Q * kWave + lane];
                 L[Q] = max(wave_incl_scan(m, 0u, mx), carry);
                 carry = readlane_u32(L[Q], kWave - 1);
             });
             for (uint32_t w = lane; w < kSpan / 2; w += kWave) ((uint32_t *)pmk)[w] = 0;
-            uint32_t c[kQ], row[kQ], slot[kQ];
-            S v[kQ], a[kQ];
-            sfor<kQ>([&](auto Q) {
+            uint32_t c[kLanePG], row[kLanePG], slot[kLanePG];
+            S v[kLanePG], a[kLanePG];
+            sfor<kLanePG>([&](auto Q) {
                 const uint32_t t = t0 + Q * kWave + lane;
                 c[Q] = kSent;
                 v[Q] = a[Q] = S(0);
@@ -267,60 +277,100 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
                     v[Q] = bv[bi];
                 }
             });
-            sfor<kQ>([&](auto Q) {
+            sfor<kLanePG>([&](auto Q) {
                 if (c[Q] != kSent && slot[Q] < kLaneCap) {
-                    skey[slot[Q] * kLaneRows + row[Q]] = (c[Q] << 6) | slot[Q];
-                    sval[slot[Q] * kLaneRows + row[Q]] = Sem::prod(a[Q], v[Q]);
+                    skey[slot[Q] * kQR + row[Q]] = (c[Q] << 6) | slot[Q];
+                    sval[slot[Q] * kQR + row[Q]] = Sem::prod(a[Q], v[Q]);
                 }
             });
             wave_sync();
         }
         fcarry += stot;
-        pc.mark(2);  // products into the slot table
     }
 
-    // 3. the lane's row: its slots sorted in registers, equal columns summed
-    const uint32_t cnt = lane < nt ? rcnt[lane] : 0u;
+    // 3. each row's keys sorted by its quad (lane 4r + q: row r, elements q * NL ..), then written
+    //    back row-major; lane q = 0 of the quad reads its row's N sorted keys into registers
+    const uint32_t r = lane >> 2, q = lane & 3u;
+    const uint32_t cnt = r < nt ? rcnt[r] : 0u;
     if (cnt > kLaneCap)  // the host runs the call through the pipeline instead
         __hip_atomic_store(&p.host_out[3], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t cn = cnt > kLaneCap ? 0u : cnt;
     const uint32_t wmax = wave_max_u32(cn);
-    // sorted once (network size by the wave's longest row); the non-zero count first, then the
-    // wave's offset, then the outputs from the same registers
-    auto body = [&](auto ntag) {
-        constexpr int N = decltype(ntag)::value;
-        uint32_t k[kLaneCap];
+    uint32_t nz = 0, zeros = 0, roff = 0;  // (q = 0 lanes) distinct columns, zero sums, offset in the wave
+    uint32_t k[kLaneCap];
+    auto sort_and_count = [&](auto ntag) {
+        constexpr int N = decltype(ntag)::value, NL = N / 4;
+        uint32_t kk[kLaneCap / 4];
 #pragma unroll
-        for (int s = 0; s < N; ++s) k[s] = (uint32_t)s < cn ? skey[s * kLaneRows + lane] : kSent;
-        pc.mark(3);
-        lane_sort<N>(k);
-        pc.mark(4);  // the sort
-        const S *sv = sval + lane;  // slot s of this lane's row at sv[s * kLaneRows]
-        const uint32_t nz = lane_count<N>(k);  // structural: zero sums are dropped afterwards
-        pc.mark(5);  // the count pass
-        // 4. the wave's offset (look-back over the earlier blocks), row_ptr, the rows' outputs
-        const uint32_t incl = wave_incl_scan(nz, 0u, plus);
-        const uint32_t agg = readlane_u32(incl, kWave - 1);
-        const uint32_t rmax = wave_max_u32(nz);
-        // (the max row first, its result waited for: it is in place once a later block sees this
-        // block's status, so the last block reads the final max after its look-back)
-        if (lane == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | rmax));
-        // the aggregate published first; u32 rows then stage their outputs in LDS at the wave-local
-        // offset while the earlier blocks finish, and only the coalesced store waits for the offset
-        lookback_publish(status, blockIdx.x, epoch, agg);
-        uint32_t zeros = 0;
-        if constexpr (sizeof(S) == 4) {
-            const uint32_t o0 = incl - nz;
-            if (nz)
-                zeros = lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
-                    skey[o0 + j] = col;
-                    stg[o0 + j] = val;
-                });
-            wave_sync();
+        for (int j = 0; j < NL; ++j) {
+            const uint32_t e = q * NL + (uint32_t)j;
+            kk[j] = e < cn ? skey[e * kQR + r] : kSent;
         }
-        pc.mark(7);  // (u32) the outputs staged
+        quad_sort<NL>(kk, q);
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < NL; ++j) skey[r * kLaneCap + q * NL + (uint32_t)j] = kk[j];
+        wave_sync();
+        if (q == 0) {
+#pragma unroll
+            for (int e = 0; e < N; ++e) k[e] = skey[r * kLaneCap + (uint32_t)e];
+#pragma unroll
+            for (int e = N; e < (int)kLaneCap; ++e) k[e] = kSent;
+            // distinct columns (structural: zero sums are dropped afterwards)
+#pragma unroll
+            for (int e = 0; e < N; ++e) nz += (k[e] != kSent && (e == 0 || (k[e] >> 6) != (k[e - 1] >> 6))) ? 1u : 0u;
+        }
+    };
+    if (wmax <= 16)
+        sort_and_count(std::integral_constant<int, 16>{});
+    else if (wmax <= 32)
+        sort_and_count(std::integral_constant<int, 32>{});
+    else
+        sort_and_count(std::integral_constant<int, 64>{});
+    const uint32_t wincl = wave_incl_scan(nz, 0u, plus);
+    roff = wincl - nz;
+    const uint32_t wsum = readlane_u32(wincl, kWave - 1);
+    if (lane == 0) s_wsum[wv] = wsum;
+    const uint32_t rmax = wave_max_u32(nz);
+    if (lane == 0 && rmax) atomicMax(s_max, rmax);
+    __syncthreads();
+    // 4. the block's aggregate published first; u32 rows then stage their outputs in LDS at the
+    //    block-local offset while the earlier blocks finish, and only the coalesced store waits for
+    //    the offset (decoupled look-back over the earlier blocks' status words)
+    uint32_t wbase = 0, agg = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kLaneWaves; ++w) {
+        const uint32_t x = s_wsum[w];
+        wbase += w < wv ? x : 0u;
+        agg += x;
+    }
+    if (threadIdx.x == 0) {
+        // the max row first, its result waited for: it is in place once a later block sees this
+        // block's status, so the last block reads the final max after its look-back
+        pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | *s_max));
+        lookback_publish(status, blockIdx.x, epoch, agg);
+    }
+    const S *sv = sval + r;  // slot e of this lane's row at sv[e * kQR]
+    if constexpr (sizeof(S) == 4) {
+        if (q == 0 && nz) {
+            const uint32_t o0 = wbase + roff;
+            auto emit = [&](uint32_t col, S val, uint32_t j) {
+                stc[o0 + j] = col;
+                stv[o0 + j] = val;
+            };
+            if (wmax <= 16)
+                zeros = lane_combine<Sem, 16>(k, sv, emit);
+            else if (wmax <= 32)
+                zeros = lane_combine<Sem, 32>(k, sv, emit);
+            else
+                zeros = lane_combine<Sem, 64>(k, sv, emit);
+        }
+    }
+    __syncthreads();
+    if (wv == 0) {
         const unsigned long long excl = lookback_walk(status, blockIdx.x, epoch, agg);
         if (lane == 0) {
+            *s_off = excl;
             if (blockIdx.x == gridDim.x - 1) {
                 const unsigned long long mw = __hip_atomic_load(maxw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long mxr = (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull;
@@ -331,49 +381,41 @@ __global__ __launch_bounds__(kWave) void k_lane(Args p, unsigned long long *stat
                 asm volatile("" ::"v"(o0), "v"(o1));
             }
         }
-        pc.mark(6);  // look-back
-        const uint64_t base = excl + (incl - nz);
-        if (lane < nt) {
-            p.c_rp[r + 1] = base + nz;
-            if (r == 0) p.c_rp[0] = 0;
-        }
-        if constexpr (sizeof(S) == 4) {
-            // the wave's rows are contiguous in C: the staged outputs stored coalesced (scattered
-            // per-lane stores cost one instruction per output)
-            uint32_t *oc = p.c_col + excl;
-            S *ov = (S *)p.c_val + excl;
-            for (uint32_t u = lane; u < agg; u += kWave) {
-                oc[u] = skey[u];
-                ov[u] = stg[u];
-            }
-        } else if (nz) {
-            uint32_t *oc = p.c_col + base;
-            S *ov = (S *)p.c_val + base;
-            zeros = lane_combine<Sem, N>(k, sv, [&](uint32_t col, S val, uint32_t j) {
-                oc[j] = col;
-                ov[j] = val;
-            });
-        }
-        // zero sums (explicit zero inputs, f64 cancellation) stay in C for now: the row's non-zero
-        // count goes to p.counts and the rows with zeros to host_out[2], and the host compacts
-        // (as after k_numeric)
-        if (lane < nt) p.counts[r] = nz - zeros;
-        add_zero_rows(&p.host_out[2], wave_sum_u32(zeros ? 1u : 0u), true);
-        pc.mark(8);  // row_ptr, the emit
-    };
-    if (wmax <= 16)
-        body(std::integral_constant<int, 16>{});
-    else if (wmax <= 32)
-        body(std::integral_constant<int, 32>{});
-    else
-        body(std::integral_constant<int, 64>{});
-    if constexpr (SLAT_PHASES) {
-        pc.ph[kPhaseSlots - 1] = 1;  // waves
-        if (lane == 0) {
-            unsigned long long *dst = p.shards + 512 + (blockIdx.x % 64) * kPhaseSlots;
-            for (int i = 0; i < kPhaseSlots; ++i) atomicAdd(&dst[i], (unsigned long long)pc.ph[i]);
-        }
     }
+    __syncthreads();
+    const unsigned long long excl = *s_off;
+    const uint64_t base = excl + wbase + roff;  // (q = 0 lanes) the row's first output
+    if (q == 0 && r < nt) {
+        p.c_rp[r0 + r + 1] = base + nz;
+        if (r0 + r == 0) p.c_rp[0] = 0;
+    }
+    if constexpr (sizeof(S) == 4) {
+        // the block's rows are contiguous in C: the staged outputs stored coalesced
+        uint32_t *oc = p.c_col + excl;
+        S *ov = (S *)p.c_val + excl;
+        for (uint32_t u = threadIdx.x; u < agg; u += kLaneWaves * kWave) {
+            oc[u] = stc[u];
+            ov[u] = stv[u];
+        }
+    } else if (q == 0 && nz) {
+        uint32_t *oc = p.c_col + base;
+        S *ov = (S *)p.c_val + base;
+        auto emit = [&](uint32_t col, S val, uint32_t j) {
+            oc[j] = col;
+            ov[j] = val;
+        };
+        if (wmax <= 16)
+            zeros = lane_combine<Sem, 16>(k, sv, emit);
+        else if (wmax <= 32)
+            zeros = lane_combine<Sem, 32>(k, sv, emit);
+        else
+            zeros = lane_combine<Sem, 64>(k, sv, emit);
+    }
+    // zero sums (explicit zero inputs, f64 cancellation) stay in C for now: the row's non-zero count
+    // goes to p.counts and the rows with zeros to host_out[2], and the host compacts (as after
+    // k_numeric)
+    if (q == 0 && r < nt) p.counts[r0 + r] = nz - zeros;
+    add_zero_rows(&p.host_out[2], wave_sum_u32(zeros ? 1u : 0u), true);
     signal_done(p);
 }
 
@@ -381,12 +423,12 @@ template <typename Sem>
 hipError_t launch(dim3 grid, hipStream_t s, const Args &a, unsigned long long *status, uint32_t epoch,
                   unsigned long long *maxw) {
     constexpr size_t lds = lane_lds<typename Sem::S>();
-    static bool attr = false;  // > 64 KB of dynamic LDS is not needed (<= 53 KB); set once anyway
+    static bool attr = false;  // over 64 KB of dynamic LDS (u32: ~70 KB, two blocks per CU)
     if (!attr) {
         (void)hipFuncSetAttribute((const void *)k_lane<Sem>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr = true;
     }
-    hipLaunchKernelGGL(k_lane<Sem>, grid, dim3(kWave), lds, s, a, status, epoch, maxw);
+    hipLaunchKernelGGL(k_lane<Sem>, grid, dim3(kLaneWaves * kWave), lds, s, a, status, epoch, maxw);
     return hipGetLastError();
 }
 

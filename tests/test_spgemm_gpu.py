@@ -559,3 +559,37 @@ def test_lane_rows(ctx, dtype, case):
         # the pair is remembered: the next call goes to the pipeline without the lane attempt
         assert_same(da._spgemm(db), want, "overflow, second call")
         assert not ctx.stats()["mode"] & 8, "the remembered pair ran the lane kernel again"
+
+
+@pytest.mark.parametrize("ncols", [(1 << 26) - 1, 1 << 26])
+def test_lane_sort_key_column_limit(ctx, ncols):
+    # The lane kernel's sort key is (column << 6) | slot; with 2^26 columns the last column at slot 63
+    # would equal the padding key 0xFFFFFFFF and the product would be dropped, so the kernel takes
+    # only n_cols < 2^26. A row of 64 products, all in the last column: its sum
+    # must be 64 whichever path runs (rectangular views through the C ABI: 1 x 64 times 64 x ncols)
+    import ctypes as C
+    from slat import _lib as L
+    last = ncols - 1
+
+    def host_view(n_rows, n_cols, rp, col, val):
+        v = L.CsrView()
+        v.n_rows, v.n_cols, v.nnz = n_rows, n_cols, len(col)
+        v.row_ptr, v.col_idx, v.values = rp.ctypes.data, col.ctypes.data, val.ctypes.data
+        v.dtype, v.residency = slat.U32, L.HOST
+        v.max_row_nnz = int(np.diff(rp.astype(np.int64)).max(initial=0))
+        return v
+    arp, acol, aval = np.array([0, 64], np.uint64), np.arange(64, dtype=np.uint32), np.ones(64, np.uint32)
+    brp, bcol, bval = np.arange(65, dtype=np.uint64), np.full(64, last, np.uint32), np.ones(64, np.uint32)
+    va, vb = host_view(1, 64, arp, acol, aval), host_view(64, ncols, brp, bcol, bval)
+    out = L.CsrOwned()
+    L.check(L.lib().slat_spgemm(ctx.ptr, C.byref(va), C.byref(vb), C.byref(out), 0), ctx.ptr)
+    try:
+        lane_ran = bool(ctx.stats()["mode"] & 8)
+        assert int(out.nnz) == 1
+        rp, col, val = np.empty(2, np.uint64), np.empty(1, np.uint32), np.empty(1, np.uint32)
+        v = L.lib().slat_csr_view_of(C.byref(out))
+        L.check(L.lib().slat_csr_to_host(ctx.ptr, C.byref(v), rp.ctypes.data, col.ctypes.data, val.ctypes.data), ctx.ptr)
+        assert int(col[0]) == last and int(val[0]) == 64, (col, val)
+        assert lane_ran == (ncols < (1 << 26))
+    finally:
+        L.lib().slat_csr_free(ctx.ptr, C.byref(out))
