@@ -487,12 +487,11 @@ slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, 
     slat_status st;
     if ((st = ensure_status(ctx, tiles, s))) return st;
     const uint32_t epoch = slat_next_scan_epoch(ctx, s);
-    const bool ticketed = tiles > (uint64_t)ctx->cu_count;
-    hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)tiles), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status,
-                       ticketed ? ctx->d_words + 1 : nullptr, ctx->ticket_base, epoch, ctx->d_words + 2,
-                       ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch, bmax, nbmax);
+    // at most one block per CU, each taking its tiles in order (k_scan_rows)
+    const uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)ctx->cu_count);
+    hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)grid), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status, epoch,
+                       ctx->d_words + 2, ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch, bmax, nbmax);
     SLAT_HIP(ctx, hipGetLastError());
-    if (ticketed) ctx->ticket_base += tiles;
     return SLAT_OK;
 }
 
@@ -1155,7 +1154,14 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         if (all_short) {
             // (no listed rows)
         } else {
-            SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, sym_grid, sym_lds, s, h2));
+            // the listed rows take tickets in wide launches, so a resident grid covers any list (the
+            // launch is mostly its dispatch when the list is short: C4 lists none, and 4 096 blocks
+            // took 4.8 us to dispatch)
+            dim3 g2 = sym_grid;
+            if (h2.tq)
+                g2.x = (unsigned)std::min<uint64_t>(g2.x, (uint64_t)ctx->cu_count *
+                                                              slat_symbolic_listed_blocks_per_cu(idx32, ell, sym_lds));
+            SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, g2, sym_lds, s, h2));
         }
         a.list = all_short ? nullptr : (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
         a.list_cnt = all_short ? nullptr : lc + 2;

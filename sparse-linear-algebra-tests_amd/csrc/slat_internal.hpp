@@ -42,7 +42,7 @@ struct slat_ctx {
     unsigned long long *h_out_dev = nullptr; // its device alias (written by k_scan_rows / k_numeric); [7]: the
                                              // end-of-call sequence word (k_signal)
     unsigned long long done_seq = 0;         // last sequence number queued to [7]
-    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] scan ticket, [2] max-row word, [3] ~min-B word,
+    unsigned long long *d_words = nullptr;   // [0] max-B word, [1] unused, [2] max-row word, [3] ~min-B word,
                                              // [4] check flags, [5] work tickets (zeroed by each launch's last taker),
                                              // [6] unused, [8] / [10] the short-row kernels' list lengths
                                              // (tagged list_epoch),
@@ -61,7 +61,6 @@ struct slat_ctx {
     uint32_t lane_miss_next = 0;
     unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
     uint64_t status_cap = 0;                 // tiles d_status holds
-    unsigned long long ticket_base = 0;      // tiles handed out so far (the ticket is monotonic)
     uint32_t scan_epoch = 0;                 // tag of the status / max-row words (22 bits)
     size_t free_b = 0;                       // cached hipMemGetInfo free bytes
     uint32_t free_age = 0;

@@ -61,6 +61,8 @@ hipError_t slat_launch_tiny(int sem, dim3 grid, size_t lds, hipStream_t s, const
 hipError_t slat_launch_symbolic_short(bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s, const slat::Args &a);
 // resident 256-thread blocks per CU of that instance at `lds` bytes (cached per thread)
 int slat_symbolic_short_blocks_per_cu(bool idx32, bool ell, size_t lds);
+// resident blocks per CU of the listed-row (window) symbolic instance, mode 2
+int slat_symbolic_listed_blocks_per_cu(bool idx32, bool ell, size_t lds);
 
 
 // rows of at most slat_lane_cap() products in one kernel, a row per lane (slat_lane.hip): n rows in

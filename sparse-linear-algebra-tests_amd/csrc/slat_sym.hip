@@ -55,3 +55,18 @@ int slat_symbolic_short_blocks_per_cu(bool idx32, bool ell, size_t lds) {
     cache_nb[ci] = nb;
     return nb;
 }
+
+int slat_symbolic_listed_blocks_per_cu(bool idx32, bool ell, size_t lds) {
+    static thread_local int cache_nb[4] = {};
+    static thread_local size_t cache_lds[4] = {};
+    const int ci = (idx32 ? 1 : 0) | (ell ? 2 : 0);
+    if (cache_lds[ci] == lds && cache_nb[ci] > 0) return cache_nb[ci];
+    int nb = 0;
+    auto q = [&](auto kern) { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, kBlock, lds); };
+    const hipError_t e = idx32 ? (ell ? q(k_symbolic<uint32_t, true, 2>) : q(k_symbolic<uint32_t, false, 2>))
+                               : (ell ? q(k_symbolic<uint64_t, true, 2>) : q(k_symbolic<uint64_t, false, 2>));
+    nb = (e == hipSuccess && nb > 0) ? nb : 1;
+    cache_lds[ci] = lds;
+    cache_nb[ci] = nb;
+    return nb;
+}

@@ -2759,8 +2759,8 @@ void k_numeric_short_u32(Args p) {
 
 // ------------------------------------------------------------------------------------------------
 // row_ptr = inclusive scan of the row counts: ONE single-pass kernel (decoupled look-back). Tiles of
-// 2048 rows are taken in ticket order (a monotonic counter, so no reset), each publishes its
-// aggregate then its inclusive prefix in an epoch-tagged status word (no init kernel). The last
+// 2048 rows, each publishes its aggregate then its inclusive prefix in an epoch-tagged status word
+// (no init kernel). The last
 // tile writes the total nnz and the max row nnz into mapped host memory (no copy in the stream).
 // ------------------------------------------------------------------------------------------------
 #ifndef SLAT_SCAN_THREADS
@@ -2862,9 +2862,13 @@ __device__ __forceinline__ unsigned long long lookback_prefix_wave(unsigned long
 // bpart (optional): k_build_ell's nbpart per-block B-value partials ((~min << 32) | max), reduced by
 // one wave of tile 0 into vmax[kVMaxWord] = (vepoch << 32) | max, vmax[kVMinInvWord] =
 // (vepoch << 32) | ~min for the numeric pass (which runs after this kernel)
+// Tiles in increasing order per block: block b takes tiles b, b + G, b + 2G, ... (G = the grid,
+// at most one block per CU, all resident), so every tile's predecessors belong to blocks that are
+// running or done, and the walk back from tile t finds tile t - G's inclusive prefix within one round
+// of 256 predecessors. (Ticket order, used before for grids past the CU count, took one atomic on a
+// single address per tile: C4's 489 tiles took 23 us for an 8 MB scan.)
 static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_t *counts, uint64_t n, uint64_t *rp,
-                                                            unsigned long long *status, unsigned long long *ticket,
-                                                            unsigned long long ticket_base, uint32_t epoch,
+                                                            unsigned long long *status, uint32_t epoch,
                                                             unsigned long long *maxw, unsigned long long *host_out,
                                                             const unsigned long long *bpart, uint32_t nbpart,
                                                             unsigned long long *vmax, uint32_t vepoch,
@@ -2875,87 +2879,82 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
     const int t = threadIdx.x, lane = lane_id(), w = t / kWave;
     const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
     auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    // tiles in ticket order; a grid that is resident at once (ticket = null: at most one block per
-    // CU) takes blockIdx order instead, one memory round trip less
-    uint64_t tile = blockIdx.x;
-    if (ticket) {
-        if (t == 0) s_bcast[0] = atomicAdd(ticket, 1ull) - ticket_base;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        // bmax (<= 16 * kScanThreads entries): the counts' producer left per-block max counts; the
+        // last tile reduces them, its loads issued now so they land during the look-back
+        uint32_t bm = 0;
+        if (bmax && tile == ntiles - 1) {
+            uint32_t q[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t i = (uint32_t)t + (uint32_t)k * kScanThreads;
+                q[k] = i < nbmax ? bmax[i] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) bm = max(bm, q[k]);
+        }
+        const uint64_t i0 = tile * kScanTile + (uint64_t)t * kScanItems;
+        unsigned long long v[kScanItems], run = 0;
+        uint32_t mx = 0;
+#pragma unroll
+        for (int e = 0; e < kScanItems; ++e) v[e] = i0 + e < n ? counts[i0 + e] : 0ull;
+#pragma unroll
+        for (int e = 0; e < kScanItems; ++e) {
+            mx = max(mx, (uint32_t)min<unsigned long long>(v[e], 0xFFFFFFFFull));
+            run += v[e];
+            v[e] = run;
+        }
+        const unsigned long long wi = wave_incl_scan_u64(run);
+        mx = wave_max_u32(bmax ? bm : mx);
+        if (lane == kWave - 1) wsum[w] = wi;
+        if (lane == 0) wmax[w] = mx;
         __syncthreads();
-        tile = s_bcast[0];
-    }
-    // bmax (<= 16 * kScanThreads entries): the counts' producer left per-block max counts; the last
-    // tile reduces them, its loads issued now so they land during the look-back
-    uint32_t bm = 0;
-    if (bmax && tile == ntiles - 1) {
-        uint32_t q[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t i = (uint32_t)t + (uint32_t)k * kScanThreads;
-            q[k] = i < nbmax ? bmax[i] : 0u;
+        unsigned long long wpre = 0, agg = 0;
+        for (int k = 0; k < kScanThreads / kWave; ++k) {
+            const unsigned long long x = wsum[k];
+            wpre += k < w ? x : 0ull;
+            agg += x;
         }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) bm = max(bm, q[k]);
-    }
-    const uint64_t i0 = tile * kScanTile + (uint64_t)t * kScanItems;
-    unsigned long long v[kScanItems], run = 0;
-    uint32_t mx = 0;
-#pragma unroll
-    for (int e = 0; e < kScanItems; ++e) v[e] = i0 + e < n ? counts[i0 + e] : 0ull;
-#pragma unroll
-    for (int e = 0; e < kScanItems; ++e) {
-        mx = max(mx, (uint32_t)min<unsigned long long>(v[e], 0xFFFFFFFFull));
-        run += v[e];
-        v[e] = run;
-    }
-    const unsigned long long wi = wave_incl_scan_u64(run);
-    mx = wave_max_u32(bmax ? bm : mx);
-    if (lane == kWave - 1) wsum[w] = wi;
-    if (lane == 0) wmax[w] = mx;
-    __syncthreads();
-    unsigned long long wpre = 0, agg = 0;
-    for (int k = 0; k < kScanThreads / kWave; ++k) {
-        const unsigned long long x = wsum[k];
-        wpre += k < w ? x : 0ull;
-        agg += x;
-    }
-    if (w == 0) {
-        uint32_t m = 0;
-        for (int k = 0; k < kScanThreads / kWave; ++k) m = max(m, wmax[k]);
-        // max row first (its result waited for), then the status: the max is in place once any
-        // later tile sees this tile's status (bmax: the last tile has it from the producer's maxima)
-        if (!bmax && lane == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
-        // the walk by the whole wave, 64 predecessors per round: a lane-0 walk was one dependent
-        // load per predecessor still holding only its aggregate (one rank's eighth of C4, 62 tiles:
-        // 18.8 us for a 1 MB scan)
-        const unsigned long long excl = lookback_prefix_wave(status, tile, epoch, agg);
-        if (lane == 0) s_bcast[1] = excl;
-        if (lane == 0 && tile == ntiles - 1) {
-            if (n > 0) rp[0] = 0;
-            const unsigned long long mw = bmax ? 0ull : ld(maxw);
-            const unsigned long long out[2] = {excl + agg, bmax ? (unsigned long long)m
-                                                                : (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull};
-            for (int k = 0; k < 2; ++k)
-                __hip_atomic_store(&host_out[k], out[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (w == 0) {
+            uint32_t m = 0;
+            for (int k = 0; k < kScanThreads / kWave; ++k) m = max(m, wmax[k]);
+            // max row first (its result waited for), then the status: the max is in place once any
+            // later tile sees this tile's status (bmax: the last tile has it from the producer's maxima)
+            if (!bmax && lane == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
+            // the walk by the whole wave, 256 predecessors per round: a lane-0 walk was one dependent
+            // load per predecessor still holding only its aggregate (one rank's eighth of C4, 62
+            // tiles: 18.8 us for a 1 MB scan)
+            const unsigned long long excl = lookback_prefix_wave(status, tile, epoch, agg);
+            if (lane == 0) s_bcast[1] = excl;
+            if (lane == 0 && tile == ntiles - 1) {
+                if (n > 0) rp[0] = 0;
+                const unsigned long long mw = bmax ? 0ull : ld(maxw);
+                const unsigned long long out[2] = {excl + agg, bmax ? (unsigned long long)m
+                                                                    : (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull};
+                for (int k = 0; k < 2; ++k)
+                    __hip_atomic_store(&host_out[k], out[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
-    }
-    __syncthreads();
-    const unsigned long long pre = s_bcast[1] + wpre + (wi - run);
+        __syncthreads();
+        const unsigned long long pre = s_bcast[1] + wpre + (wi - run);
 #pragma unroll
-    for (int e = 0; e < kScanItems; ++e)
-        if (i0 + e < n) rp[1 + i0 + e] = pre + v[e];
-    if (tile == 0 && nbpart && w == kScanThreads / kWave - 1) {
-        uint32_t bx = 0, bn = 0;  // max, max of ~min
-        for (uint32_t i = lane; i < nbpart; i += kWave) {
-            const unsigned long long q = bpart[i];
-            bx = max(bx, (uint32_t)q);
-            bn = max(bn, (uint32_t)(q >> 32));
+        for (int e = 0; e < kScanItems; ++e)
+            if (i0 + e < n) rp[1 + i0 + e] = pre + v[e];
+        if (tile == 0 && nbpart && w == kScanThreads / kWave - 1) {
+            uint32_t bx = 0, bn = 0;  // max, max of ~min
+            for (uint32_t i = lane; i < nbpart; i += kWave) {
+                const unsigned long long q = bpart[i];
+                bx = max(bx, (uint32_t)q);
+                bn = max(bn, (uint32_t)(q >> 32));
+            }
+            bx = wave_max_u32(bx);
+            bn = wave_max_u32(bn);
+            if (lane == 0) {
+                vmax[kVMaxWord] = ((unsigned long long)vepoch << 32) | bx;
+                vmax[kVMinInvWord] = ((unsigned long long)vepoch << 32) | bn;
+            }
         }
-        bx = wave_max_u32(bx);
-        bn = wave_max_u32(bn);
-        if (lane == 0) {
-            vmax[kVMaxWord] = ((unsigned long long)vepoch << 32) | bx;
-            vmax[kVMinInvWord] = ((unsigned long long)vepoch << 32) | bn;
-        }
+        __syncthreads();  // (the LDS words are reused by the block's next tile)
     }
 }
 
