@@ -482,7 +482,7 @@ static slat_status ensure_status(slat_ctx *ctx, uint64_t tiles, hipStream_t s) {
 
 slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s,
                              const unsigned long long *bpart, uint32_t nbpart, uint32_t vepoch, const uint32_t *bmax,
-                             uint32_t nbmax) {
+                             uint32_t nbmax, unsigned int *zero_word) {
     const uint64_t tiles = std::max<uint64_t>((n + kScanTile - 1) / kScanTile, 1);
     slat_status st;
     if ((st = ensure_status(ctx, tiles, s))) return st;
@@ -490,7 +490,7 @@ slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, 
     // at most one block per CU, each taking its tiles in order (k_scan_rows)
     const uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)ctx->cu_count);
     hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)grid), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status, epoch,
-                       ctx->d_words + 2, ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch, bmax, nbmax);
+                       ctx->d_words + 2, ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch, bmax, nbmax, zero_word);
     SLAT_HIP(ctx, hipGetLastError());
     return SLAT_OK;
 }
@@ -1135,15 +1135,25 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     uint32_t sym_blocks = sym_grid.x;  // blocks of the symbolic launch whose maxima the scan reduces
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[0], s));
     if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return failc(st);
+    unsigned int *list_next = nullptr;  // (batched wide launches) the word the scan zeroes for the next call
     if (sym_batched) {
         // MAGNUS categorisation: the short rows batched in hash tables (k_symbolic_short bounds each
         // row's products per tile, listing the rest), then the listed rows by windows
-        // the lists' lengths: epoch-tagged words of the context (d_words[8] symbolic, [10] numeric),
-        // no clear per call
-        unsigned long long *lc = all_short ? nullptr : ctx->d_words + 8;
-        const uint32_t lep = ++ctx->list_epoch ? ctx->list_epoch : ++ctx->list_epoch;  // (0 never: a zeroed word)
+        // the lists' lengths: context words that are zero when the call starts, no memset launch:
+        // the symbolic list in one of two words alternating by call (the scan of this call zeroes
+        // the other one for the next call), the numeric list's word zeroed by k_symbolic_short's
+        // block 0. A call that stopped between its symbolic launch and its scan leaves the words
+        // dirty: the next one clears them first
+        unsigned int *lc = nullptr;
+        if (!all_short) {
+            if (ctx->lists_dirty) SLAT_HIPC(hipMemsetAsync(ctx->d_words + 8, 0, 4 * 8, s));
+            lc = (unsigned int *)(ctx->d_words + 8 + 2 * (ctx->list_parity & 1u));
+            list_next = (unsigned int *)(ctx->d_words + 8 + 2 * ((ctx->list_parity + 1) & 1u));
+            ++ctx->list_parity;
+            ctx->lists_dirty = true;
+        }
         Args h1 = asym, h2 = asym;
-        h1.list_epoch = h2.list_epoch = a.list_epoch = lep;
+        h1.list_reset = all_short ? nullptr : (unsigned int *)(ctx->d_words + 12);
         h1.cbits = a.cbits;
         h1.list = h2.list = all_short ? nullptr : (uint32_t *)(ws + o_l1);
         h1.list_cnt = h2.list_cnt = lc;
@@ -1164,7 +1174,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
             SLAT_HIPC(slat_launch_symbolic(2, idx32, ell, g2, sym_lds, s, h2));
         }
         a.list = all_short ? nullptr : (uint32_t *)(ws + o_l2);  // the numeric pass's window rows
-        a.list_cnt = all_short ? nullptr : lc + 2;
+        a.list_cnt = all_short ? nullptr : (unsigned int *)(ctx->d_words + 12);
     } else if (hash) {
         Args h1 = asym;
         h1.tq = (kDyn & 2u) ? tq : nullptr;
@@ -1182,8 +1192,9 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     const bool bpart = bell && dt != SLAT_F64;
     if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
                                bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
-                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch, asym.bmax, sym_blocks)))
+                               bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch, asym.bmax, sym_blocks, list_next)))
         return failc(st);
+    if (list_next) ctx->lists_dirty = false;  // the next call's symbolic list word is zeroed in the stream
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[2], s));
 
     if (exact) {

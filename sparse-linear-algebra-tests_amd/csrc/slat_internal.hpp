@@ -44,12 +44,13 @@ struct slat_ctx {
     unsigned long long done_seq = 0;         // last sequence number queued to [7]
     unsigned long long *d_words = nullptr;   // [0] max-B word, [1] unused, [2] max-row word, [3] ~min-B word,
                                              // [4] check flags, [5] work tickets (zeroed by each launch's last taker),
-                                             // [6] unused, [8] / [10] the short-row kernels' list lengths
-                                             // (tagged list_epoch),
+                                             // [6] unused, [8] / [10] the symbolic list length (alternating
+                                             // by call), [12] the numeric list length,
     unsigned long long *d_done = nullptr;    // the call's last kernel's two-level done count (signal_done)
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
-    uint32_t list_epoch = 0;                 // per-call tag of the list lengths d_words[8] / [10]
+    uint32_t list_parity = 0;                // which of d_words[8] / [10] the next batched call's symbolic list uses
+    bool lists_dirty = false;                // a call stopped before its scan zeroed the other list word
     // (A, B, row block) triples whose lane-kernel attempt overflowed (a row past slat_lane_cap()
     // products): the next call on the same triple goes to the pipeline directly instead of running
     // both. Keyed by both operands' arrays, sizes and the row range; an entry whose array the context
@@ -169,7 +170,7 @@ slat_status slat_check_view(slat_ctx *ctx, const slat_csr_view *v, const char *n
 // clears them on wrap)
 slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, uint64_t *rp, hipStream_t s,
                              const unsigned long long *bpart = nullptr, uint32_t nbpart = 0, uint32_t vepoch = 0,
-                             const uint32_t *bmax = nullptr, uint32_t nbmax = 0);
+                             const uint32_t *bmax = nullptr, uint32_t nbmax = 0, unsigned int *zero_word = nullptr);
 uint32_t slat_next_scan_epoch(slat_ctx *ctx, hipStream_t s);
 
 // StdRng stream position (host_gen.cpp): key words and the index of the next keystream word; and

@@ -126,10 +126,12 @@ struct Args {
     // rows of the window category, appended by the short-row kernels (symbolic / numeric lists)
     // and walked by the MODE 2 launches instead of every row
     uint32_t *list;
-    // the list's length, epoch-tagged ((list_epoch << 32) | count; another tag reads as 0), so no
-    // per-call clear (a memset launch: 4.8 us of a C4 row block's ~220)
-    unsigned long long *list_cnt;
-    uint32_t list_epoch;
+    // the list's length (a context word, zero when the call starts: no per-call memset launch, which
+    // was 4.8 us of a C4 row block's ~220); list_reset: a word k_symbolic_short's block 0 zeroes
+    // (the numeric list's length, appended to by a later kernel of the same call); scan_reset: the
+    // word k_scan_rows zeroes for the next call (the other of two alternating symbolic list words)
+    unsigned int *list_cnt;
+    unsigned int *list_reset;
     unsigned long long *host_out;  // mapped pinned host words: [0] nnz, [1] max row nnz, [2] rows with zeros
     uint64_t *counts;  // symbolic: structural nnz per row; numeric: non-zero nnz per row
     uint64_t *c_rp;    // C.row_ptr (n+1)
@@ -164,10 +166,9 @@ struct Args {
 
 __device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.fr_mark && p.fr_mark[row]; }
 
-// the length of the window-category list the short-row kernels appended to (their launch's tag)
+// the length of the window-category list the short-row kernels appended to
 __device__ __forceinline__ uint64_t list_len(const Args &p) {
-    const unsigned long long w = __hip_atomic_load(p.list_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (uint64_t)__builtin_amdgcn_readfirstlane((w >> 32) == p.list_epoch ? (uint32_t)w : 0u);
+    return (uint64_t)__builtin_amdgcn_readfirstlane(*(volatile unsigned int *)p.list_cnt);
 }
 
 // End of the call's last kernel (p.seq != 0): the last block to finish stores seq into the mapped host
@@ -2106,16 +2107,7 @@ __device__ __forceinline__ void list_rows(const Args &p, bool take, uint64_t r) 
     const unsigned long long m = __ballot(take);
     if (!m) return;
     unsigned int base = 0;
-    if (lane_id() == 0) {
-        // (tagged counter: a word of another call's tag counts from 0)
-        const unsigned long long tag = (unsigned long long)p.list_epoch << 32;
-        unsigned long long old = __hip_atomic_load(p.list_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nv;
-        do {
-            base = (old & ~0xFFFFFFFFull) == tag ? (unsigned int)old : 0u;
-            nv = tag | (base + (unsigned int)__popcll(m));
-        } while (!__hip_atomic_compare_exchange_strong(p.list_cnt, &old, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
-    }
+    if (lane_id() == 0) base = atomicAdd(p.list_cnt, (unsigned int)__popcll(m));
     base = __builtin_amdgcn_readfirstlane(base);
     if (take) p.list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)r;
 }
@@ -2237,7 +2229,10 @@ __global__ __launch_bounds__(kBlock) void k_symbolic_short(Args p) {
     uint32_t *marks = keys + kSymHashT, *rcnt = marks + 256, *gk = rcnt + kWave;
     uint8_t *gl = (uint8_t *)(gk + kStageG);
     if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) p.c_rp[0] = 0;
+        if (threadIdx.x == 0) {
+            p.c_rp[0] = 0;
+            if (p.list_reset) *p.list_reset = 0;  // the numeric list's length (appended to after this kernel)
+        }
         if (threadIdx.x < kShards) {
             p.shards[threadIdx.x * kShardStride + 1] = 0;
             p.shards[threadIdx.x * kShardStride + 2] = 0;
@@ -2872,8 +2867,10 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
                                                             unsigned long long *maxw, unsigned long long *host_out,
                                                             const unsigned long long *bpart, uint32_t nbpart,
                                                             unsigned long long *vmax, uint32_t vepoch,
-                                                            const uint32_t *bmax, uint32_t nbmax) {
+                                                            const uint32_t *bmax, uint32_t nbmax,
+                                                            unsigned int *zero_word) {
     __shared__ unsigned long long wsum[kScanThreads / kWave];
+    if (zero_word && blockIdx.x == 0 && threadIdx.x == 0) *zero_word = 0;  // (the next call's list length)
     __shared__ unsigned long long s_bcast[2];
     __shared__ uint32_t wmax[kScanThreads / kWave];
     const int t = threadIdx.x, lane = lane_id(), w = t / kWave;
