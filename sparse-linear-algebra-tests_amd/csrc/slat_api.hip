@@ -1002,7 +1002,11 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         const uint64_t nch1 = ((ncols + (1ull << csh) - 1) >> csh) + 1;
         if (B->n_rows * nch1 * 4 <= (256ull << 20) &&
             slat_dev_alloc(ctx, (void **)&wsplit, B->n_rows * nch1 * 4, s) == hipSuccess) {
-            if (slat_launch_splits(ctx, B->row_ptr, B->col_idx, B->n_rows, (uint32_t)nch1, csh, wsplit, s) != hipSuccess) {
+            // absolute offsets (B of < 2^32 entries): a window's walk then loads a B row's part bounds
+            // from the table alone, not also the row pointer
+            a.wsplit_abs = B->nnz < 0xFFFFFFFFull ? 1u : 0u;
+            if (slat_launch_splits(ctx, B->row_ptr, B->col_idx, B->n_rows, (uint32_t)nch1, csh, wsplit, s, a.wsplit_abs) !=
+                hipSuccess) {
                 ctx->err = "slat_launch_splits failed";
                 slat_dev_free(ctx, wsplit, s);
                 return SLAT_EHIP;
@@ -1105,12 +1109,14 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     asym.smask = a.smask;
     asym.nblk = a.nblk;
     asym.wsplit = a.wsplit;
+    asym.wsplit_abs = a.wsplit_abs;
     asym.wnch1 = a.wnch1;
     slat::FatArgs fat_args = {};
     slat::FatArgs *fa = &fat_args;
     if (fat) {
         if ((st = slat_fat_select(ctx, a, ws + o_fat, fat_min, fa))) return failc(st);
         fa->buckets = (flags & SLAT_FLAG_FAT_BUCKETS) ? 1u : 0u;
+        fa->split_abs = B->nnz < 0xFFFFFFFFull ? 1u : 0u;  // absolute offsets fit the split table's u32
         asym.fr_mark = a.fr_mark;
     }
     if (ablate & 7u) {

@@ -158,7 +158,7 @@ constexpr int kQ = 4;
 template <typename S, bool VALS, typename I, typename F>
 __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, uint32_t hi, bool all_cols, F &&fn,
                                         const uint32_t *split = nullptr, uint32_t nch1 = 0, uint32_t g0 = 0,
-                                        uint32_t g1 = 0) {
+                                        uint32_t g1 = 0, uint32_t split_abs = 0) {
     const int lane = lane_id();
     const int wv = threadIdx.x / kWave;
     const S *av = (const S *)p.a_val;
@@ -180,7 +180,7 @@ __device__ __forceinline__ void fr_walk(const Args &p, I a0, I a1, uint32_t lo, 
             bs[Q] = be[Q] = 0;
             if (k[Q] < p.b_nrows) {
                 if (split) {  // only the chunk's part of the B row: no filtering, no search
-                    const I r = (I)p.b_rp[k[Q]];
+                    const I r = split_abs ? (I)0 : (I)p.b_rp[k[Q]];
                     const uint32_t *sp = split + (uint64_t)k[Q] * nch1;
                     bs[Q] = r + (I)sp[g0];
                     be[Q] = r + (I)sp[g1];
@@ -344,8 +344,10 @@ __device__ __forceinline__ void fr_flat(const Args &p, I a0, I a1, Part &&part, 
 
 // the split table of B by accumulator chunk (FatArgs::split): thread per (row k, boundary c), a
 // binary search in the sorted row; boundary 0 is 0 and boundary nch1 - 1 the row length
+// (abs: the absolute offset in B instead, B of < 2^32 entries)
 __global__ __launch_bounds__(kBlock) void k_fr_splits(const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb,
-                                                       uint32_t nch1, uint32_t chunk_shift, uint32_t *split) {
+                                                       uint32_t nch1, uint32_t chunk_shift, uint32_t *split,
+                                                       uint32_t abs = 0) {
     const uint64_t total = nb * nch1;
     for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total; g += (uint64_t)gridDim.x * kBlock) {
         const uint64_t k = g / nch1;
@@ -364,7 +366,7 @@ __global__ __launch_bounds__(kBlock) void k_fr_splits(const uint64_t *b_rp, cons
                     hi = mid;
             }
         }
-        split[g] = (uint32_t)(hi - s);
+        split[g] = (uint32_t)(abs ? hi : hi - s);
     }
 }
 
@@ -474,7 +476,7 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                 [&](uint32_t k, I &bs, uint32_t &len) {
                     const uint32_t *sp = f.split + (uint64_t)k * f.nch1;
                     const uint32_t s0 = sp[g0];
-                    bs = (I)p.b_rp[k] + (I)s0;
+                    bs = (f.split_abs ? (I)0 : (I)p.b_rp[k]) + (I)s0;
                     len = sp[g1] - s0;
                 },
                 [&](uint32_t c, S a, S b) {
@@ -492,7 +494,7 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
             const uint32_t o = c - c0;
             Sem::acc(acc, o, Sem::prod(a, b));
             atomicOr(&bits[o >> 5], 1u << (o & 31));
-        }, f.split, f.nch1, g0, g1);
+        }, f.split, f.nch1, g0, g1, f.split_abs);
     } else if (f.split && (1u << f.gsh) * kFW == fr_chunk<Sem>()) {
         // the split table's granule is one wave's slice: each A entry's part of the B row is two
         // loads, no search. Entries with a non-empty part, in A order; the next one's B entries
@@ -514,7 +516,7 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
         auto load_part = [&](uint32_t k, I &bs, I &be) {
             bs = be = 0;
             if (k < p.b_nrows) {
-                const I r = (I)p.b_rp[k];
+                const I r = f.split_abs ? (I)0 : (I)p.b_rp[k];
                 const uint32_t *sp = f.split + (uint64_t)k * f.nch1 + g;
                 bs = r + (I)sp[0];
                 be = r + (I)sp[1];
@@ -618,7 +620,7 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                 k = p.a_col[i];
                 a = av[i];
                 if (k < p.b_nrows) {
-                    const I r = (I)p.b_rp[k];
+                    const I r = (f.split && f.split_abs) ? (I)0 : (I)p.b_rp[k];
                     if (f.split) {  // the chunk's part of the B row
                         const uint32_t *sp = f.split + (uint64_t)k * f.nch1;
                         bs = r + (I)sp[g0];
@@ -801,10 +803,10 @@ uint64_t slat_fat_min(bool flat) {
 
 // workspace bytes of the fat-row category for n rows
 hipError_t slat_launch_splits(slat_ctx *ctx, const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb, uint32_t nch1,
-                              uint32_t shift, uint32_t *split, hipStream_t s) {
+                              uint32_t shift, uint32_t *split, hipStream_t s, uint32_t abs) {
     const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb * nch1 + kBlock - 1) / kBlock,
                                                                            (uint64_t)ctx->cu_count * 16));
-    hipLaunchKernelGGL(k_fr_splits, dim3(gs), dim3(kBlock), 0, s, b_rp, b_col, nb, nch1, shift, split);
+    hipLaunchKernelGGL(k_fr_splits, dim3(gs), dim3(kBlock), 0, s, b_rp, b_col, nb, nch1, shift, split, abs);
     return hipGetLastError();
 }
 
@@ -906,8 +908,9 @@ static hipError_t fr_num(slat_ctx *ctx, const FatArgs &f, bool idx32) {
         if (slat_dev_alloc(ctx, (void **)&split, nb * (nch + 1) * 4, ctx->stream) == hipSuccess) {
             const unsigned gs = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((nb * (nch + 1) + kBlock - 1) / kBlock,
                                                                                    (uint64_t)ctx->cu_count * 16));
+            // (f.split_abs on entry: the host's permission, B has < 2^32 entries)
             hipLaunchKernelGGL(k_fr_splits, dim3(gs), dim3(kBlock), 0, ctx->stream, h.a.b_rp, h.a.b_col, nb,
-                               (uint32_t)(nch + 1), sh, split);
+                               (uint32_t)(nch + 1), sh, split, h.split_abs);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) {
                 slat_dev_free(ctx, split, ctx->stream);

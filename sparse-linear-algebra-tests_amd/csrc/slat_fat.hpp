@@ -17,9 +17,13 @@ struct FatArgs {
     // B split by column granule (numeric pass; null = none): split[k * nch1 + g] = the offset in B
     // row k of its first entry with column >= g << gsh (g = 0 .. nch1 - 1, the last = len). The
     // granule is the accumulator chunk, or for f64 in the reference's order one wave's slice of it
+    // split_abs: the entries hold absolute offsets in B (B of < 2^32 entries), so a walk loads the
+    // part's bounds from the table alone, without B's row pointer (one random cache line per A
+    // entry and chunk instead of two: C5's fold order read 50 GB in k_fr_numeric, mostly these)
     const uint32_t *split;
     uint32_t nch1;
     uint32_t gsh;
+    uint32_t split_abs;
     // products bucketed by accumulator chunk (integer semirings and f64 in any order; null = none):
     // each block's region of bcap (column, product) pairs at bcol / bval + blockIdx.x * bcap
     uint32_t *bcol;
@@ -35,9 +39,10 @@ struct FatArgs {
 }  // namespace slat
 
 // B (CSR) bucketed by column granule of 2^shift columns on stream s: split[k * nch1 + g] = the offset
-// in B row k of its first column >= g << shift, g in [0, nch1) (the last = the row's length)
+// in B row k of its first column >= g << shift, g in [0, nch1) (the last = the row's length); abs:
+// the absolute offset in B instead (B of < 2^32 entries)
 hipError_t slat_launch_splits(slat_ctx *ctx, const uint64_t *b_rp, const uint32_t *b_col, uint64_t nb, uint32_t nch1,
-                              uint32_t shift, uint32_t *split, hipStream_t s);
+                              uint32_t shift, uint32_t *split, hipStream_t s, uint32_t abs = 0);
 // products per row from which a row takes the fat-row kernels: 2048 with `flat` (B in CSR form, a
 // semiring that adds with atomics: the flattened walk), else 8192
 uint64_t slat_fat_min(bool flat);

@@ -154,6 +154,7 @@ struct Args {
     // = the offset in B row k of its first column >= g << chunk_shift(ncols) (null: none). A window
     // walks only its chunks' part of each B row instead of the whole row with a column filter
     const uint32_t *wsplit;
+    uint32_t wsplit_abs;  // its entries are absolute offsets in B (no row-pointer load per entry)
     uint32_t wnch1;
     // k_symbolic_short: a batch's product bound (0: kSymHashT * SLAT_SYM_CAP_PCT %). Single-window
     // launches take kHashT / 2, so every row it counts fits k_numeric_short's table and every row it
@@ -760,7 +761,7 @@ __device__ __forceinline__ void walk_csr(const Args &p, const uint32_t *k, const
         be[Q] = 0;
         if (k[Q] < p.b_nrows) {
             if (g1) {
-                const I r = (I)p.b_rp[k[Q]];
+                const I r = p.wsplit_abs ? (I)0 : (I)p.b_rp[k[Q]];
                 const uint32_t *sp = p.wsplit + (uint64_t)k[Q] * p.wnch1;
                 bs[Q] = r + (I)sp[g0];
                 be[Q] = r + (I)sp[g1];
