@@ -2877,6 +2877,18 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
     const int t = threadIdx.x, lane = lane_id(), w = t / kWave;
     const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
     auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    // (tile 0's last wave) k_build_ell's B-value partials, the first 8 per lane loaded now, so they
+    // land under the tile's scan instead of after it (a chain of dependent loads at the end of the
+    // kernel: 211 partials on the headline)
+    constexpr int kBP = 8;
+    unsigned long long bq[kBP];
+    const bool bred = blockIdx.x == 0 && nbpart && w == kScanThreads / kWave - 1;
+    if (bred)
+#pragma unroll
+        for (int k = 0; k < kBP; ++k) {
+            const uint32_t i = (uint32_t)lane + (uint32_t)k * kWave;
+            bq[k] = i < nbpart ? bpart[i] : 0ull;
+        }
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         // bmax (<= 16 * kScanThreads entries): the counts' producer left per-block max counts; the
         // last tile reduces them, its loads issued now so they land during the look-back
@@ -2938,9 +2950,14 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
 #pragma unroll
         for (int e = 0; e < kScanItems; ++e)
             if (i0 + e < n) rp[1 + i0 + e] = pre + v[e];
-        if (tile == 0 && nbpart && w == kScanThreads / kWave - 1) {
+        if (tile == 0 && bred) {
             uint32_t bx = 0, bn = 0;  // max, max of ~min
-            for (uint32_t i = lane; i < nbpart; i += kWave) {
+#pragma unroll
+            for (int k = 0; k < kBP; ++k) {
+                bx = max(bx, (uint32_t)bq[k]);
+                bn = max(bn, (uint32_t)(bq[k] >> 32));
+            }
+            for (uint32_t i = lane + kBP * kWave; i < nbpart; i += kWave) {
                 const unsigned long long q = bpart[i];
                 bx = max(bx, (uint32_t)q);
                 bn = max(bn, (uint32_t)(q >> 32));
