@@ -2814,28 +2814,31 @@ __device__ __forceinline__ unsigned long long lookback_walk(unsigned long long *
     // rounds of 64, each a device-scope load latency, ~7 us; now 2)
     for (int64_t j0 = (int64_t)tile - 1;; j0 -= kWave * kLookR) {
         unsigned long long x[kLookR];
+        int first = kLookR, last = kWave;
+        unsigned long long inc = 0;
         while (true) {
-            bool ok = true;
             sfor<kLookR>([&](auto I) {
                 const int64_t j = j0 - (lane * kLookR + I);
                 x[I] = 0;
                 if (j >= 0) x[I] = ld(&status[j]);
             });
+            // the lane's nearest published inclusive prefix (kLookR: none), the wave's nearest by
+            // ballot; only the statuses between this tile and that one must be published (a later
+            // tile's walk need not wait for tiles before the nearest inclusive prefix)
+            uint32_t valid = 0;
+            first = kLookR;
             sfor<kLookR>([&](auto I) {
                 const int64_t j = j0 - (lane * kLookR + I);
-                if (j >= 0) ok = ok && (x[I] >> 42) == epoch && (x[I] & (kStAgg | kStInc)) != 0;
+                const bool v = j < 0 || ((x[I] >> 42) == epoch && (x[I] & (kStAgg | kStInc)) != 0);
+                valid |= (v ? 1u : 0u) << I;
+                if (first == kLookR && j >= 0 && v && (x[I] & kStInc)) first = I;
             });
-            if (__ballot(!ok) == 0) break;
+            inc = __ballot(first < kLookR);
+            last = inc ? (int)__builtin_ctzll(inc) : kWave;  // the lane holding it (kWave: none)
+            const uint32_t need = lane < last ? (1u << kLookR) - 1 : lane == last ? (1u << first) - 1 : 0u;
+            if (__ballot((valid & need) != need) == 0) break;
             __builtin_amdgcn_s_sleep(1);
         }
-        // the lane's nearest inclusive prefix (kLookR: none), then the wave's nearest by ballot
-        int first = kLookR;
-        sfor<kLookR>([&](auto I) {
-            const int64_t j = j0 - (lane * kLookR + I);
-            if (first == kLookR && j >= 0 && (x[I] & kStInc)) first = I;
-        });
-        const unsigned long long inc = __ballot(first < kLookR);
-        const int last = inc ? (int)__builtin_ctzll(inc) : kWave;  // the lane holding it (kWave: none)
         unsigned long long v = 0;
         sfor<kLookR>([&](auto I) {
             const int64_t j = j0 - (lane * kLookR + I);
