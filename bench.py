@@ -126,10 +126,11 @@ def e2e_leg(ctx, P, A, steps: int):
         return y
     pP = slat.HostCsr(hP.n, pin(hP.row_ptr), pin(hP.col_idx), pin(hP.values), hP.dtype)
     pA = slat.HostCsr(hA.n, pin(hA.row_ptr), pin(hA.col_idx), pin(hA.values), hA.dtype)
-    pool = {}
+    pool, seq = {}, [0]
 
     def pooled(n, dt):  # a pinned output pool, one buffer per (array, size), reused across calls
-        key = (n, np.dtype(dt).str)
+        key = (seq[0] % 3, n, np.dtype(dt).str)  # (spgemm_host asks for row_ptr, col, val in turn)
+        seq[0] += 1
         if key not in pool:
             pool[key] = slat.pinned_empty(n, dt)
         return pool[key]

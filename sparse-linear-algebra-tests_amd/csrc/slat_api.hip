@@ -77,7 +77,8 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
         return SLAT_EOOM;
     }
     if (hipMalloc((void **)&ctx->d_words, 128) != hipSuccess || hipMemset(ctx->d_words, 0, 128) != hipSuccess ||
-        hipMalloc((void **)&ctx->d_done, kDoneBytes) != hipSuccess || hipMemset(ctx->d_done, 0, kDoneBytes) != hipSuccess ||
+        hipMalloc((void **)&ctx->d_done, kDoneBytes + kMaxwBytes) != hipSuccess ||
+        hipMemset(ctx->d_done, 0, kDoneBytes + kMaxwBytes) != hipSuccess ||
         hipHostMalloc((void **)&ctx->h_out, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&ctx->h_out_dev, ctx->h_out, 0) != hipSuccess) {
         (void)hipHostFree(ctx->h_shards);
@@ -87,6 +88,7 @@ slat_status slat_ctx_create(int device, slat_ctx **out) {
     }
     std::memset(ctx->h_out, 0, 64);  // [7] must not match the first call's sequence number
     ctx->d_vmax = ctx->d_words;
+    ctx->d_maxw = ctx->d_done + kDoneBytes / 8;  // (the one-kernel paths' max row words)
     for (auto &e : ctx->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);  // timing only
     *out = ctx;
     return SLAT_OK;
@@ -461,7 +463,7 @@ static hipError_t launch_compact(dim3 grid, hipStream_t s, const uint64_t *orp, 
 uint32_t slat_next_scan_epoch(slat_ctx *ctx, hipStream_t s) {
     if (++ctx->scan_epoch >= (1u << 22)) {  // tag wrap: clear every tagged word once
         if (ctx->d_status) (void)hipMemsetAsync(ctx->d_status, 0, ctx->status_cap * 8, s);
-        (void)hipMemsetAsync(ctx->d_words + 2, 0, 8, s);
+        (void)hipMemsetAsync(ctx->d_maxw, 0, kMaxwBytes, s);
         ctx->scan_epoch = 1;
     }
     return ctx->scan_epoch;
@@ -490,7 +492,7 @@ slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, 
     // at most one block per CU, each taking its tiles in order (k_scan_rows)
     const uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)ctx->cu_count);
     hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)grid), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status, epoch,
-                       ctx->d_words + 2, ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch, bmax, nbmax, zero_word);
+                       ctx->d_maxw, ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch, bmax, nbmax, zero_word);
     SLAT_HIP(ctx, hipGetLastError());
     return SLAT_OK;
 }
@@ -1067,7 +1069,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         const uint64_t g = row_blocks;
         if ((st = ensure_status(ctx, g, s))) return failc(st);
         const uint32_t epoch = slat_next_scan_epoch(ctx, s);
-        SLAT_HIPC(slat_launch_tiny(sem, dim3((unsigned)g), num_lds, s, a, ctx->d_status, epoch, ctx->d_words + 2));
+        SLAT_HIPC(slat_launch_tiny(sem, dim3((unsigned)g), num_lds, s, a, ctx->d_status, epoch, ctx->d_maxw));
         hc.mark(5);
         hc.mark(6);
         SLAT_HIPC(wait_stream(ctx, s, a.seq));
@@ -1084,7 +1086,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         if (timing)
             for (int i = 0; i < 3; ++i) SLAT_HIPC(hipEventRecord(ctx->ev[i], s));
         if (SLAT_PHASES) SLAT_HIPC(hipMemsetAsync(a.shards, 0, shards_b, s));
-        SLAT_HIPC(slat_launch_lane(sem, dim3((unsigned)g), s, a, ctx->d_status, epoch, ctx->d_words + 2));
+        SLAT_HIPC(slat_launch_lane(sem, dim3((unsigned)g), s, a, ctx->d_status, epoch, ctx->d_maxw));
         if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));
         hc.mark(5);
         hc.mark(6);

@@ -47,6 +47,7 @@ struct slat_ctx {
                                              // [6] unused, [8] / [10] the symbolic list length (alternating
                                              // by call), [12] the numeric list length,
     unsigned long long *d_done = nullptr;    // the call's last kernel's two-level done count (signal_done)
+    unsigned long long *d_maxw = nullptr;    // = d_done + kDoneBytes / 8: the one-kernel paths' max-row words
     unsigned long long *d_vmax = nullptr;    // = d_words + 0: (epoch << 32) | max B value (k_build_ell)
     uint32_t epoch = 0;                      // per-call tag of d_vmax (no reset between calls)
     uint32_t list_parity = 0;                // which of d_words[8] / [10] the next batched call's symbolic list uses

@@ -167,6 +167,102 @@ __device__ __forceinline__ uint32_t lane_combine(const uint32_t (&k)[kLaneCap], 
     return zeros;
 }
 
+// quad helpers (DPP quad permutes): lane q's value from quad lane CTRL picks
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, true);
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned long long quad_perm64(unsigned long long x) {
+    return ((unsigned long long)quad_perm<CTRL>((uint32_t)(x >> 32)) << 32) | quad_perm<CTRL>((uint32_t)x);
+}
+constexpr int kQPrev = 0x90, kQNext = 0xF9, kQFirst = 0x00, kQLast = 0xFF;  // [0,0,1,2] [1,2,3,3] [0,0,0,0] [3,3,3,3]
+
+// Integer semirings: the row's sorted keys stay where the sort left them, NL per quad lane, and the
+// quad counts and sums the row's columns together (a quarter of the serial work of one lane walking
+// all N keys). A key starts a column when its column differs from the key before it in row order
+// (the previous lane's last key for j = 0); the quad's prefix of the starts numbers the outputs. Each
+// lane sums its keys' values run by run: elements before its first start belong to a run from an
+// earlier lane (its head), and its last run may continue into later lanes, which is the sum of their
+// heads up to the first lane with a start of its own. Sums are exact in any order (u32: u64 sums;
+// Sat64: saturating), so the split changes nothing. f64 keeps one lane per row (the left fold).
+template <int NL>
+__device__ __forceinline__ void quad_count(const uint32_t (&kk)[kLaneCap / 4], uint32_t q, uint32_t &starts,
+                                           uint32_t &first, uint32_t &total) {
+    uint32_t prev = quad_perm<kQPrev>(kk[NL - 1]);
+    if (q == 0) prev = kSent;
+    starts = 0;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        const uint32_t pk = j == 0 ? prev : kk[j - 1];
+        const bool st = kk[j] != kSent && (pk == kSent || (pk >> 6) != (kk[j] >> 6));
+        starts |= (st ? 1u : 0u) << j;
+    }
+    const uint32_t n = __popc(starts);
+    uint32_t v = n;
+    const uint32_t v1 = quad_perm<kQPrev>(v);
+    v += q >= 1 ? v1 : 0u;
+    const uint32_t v2 = quad_perm<0x40>(v);  // [0,0,0,1]: lane q - 2
+    v += q >= 2 ? v2 : 0u;
+    first = v - n;
+    total = quad_perm<kQLast>(v);
+}
+
+template <typename Sem>
+__device__ __forceinline__ typename LaneSum<Sem>::T quad_comb(typename LaneSum<Sem>::T a, typename LaneSum<Sem>::T b) {
+    if constexpr (std::is_same_v<Sem, SemU32>)
+        return a + b;  // < 2^38
+    else
+        return a + b < a ? ~0ull : a + b;  // Saturating<u64>
+}
+
+// emit(col, value, row output index) for the lane's outputs; returns the lane's zero sums
+template <typename Sem, int NL, typename F>
+__device__ __forceinline__ uint32_t quad_combine(const uint32_t (&kk)[kLaneCap / 4], uint32_t starts, uint32_t first,
+                                                 const typename Sem::S *sv, uint32_t q, F &&emit) {
+    using S = typename Sem::S;
+    using L = LaneSum<Sem>;
+    using T = typename L::T;
+    S v[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) v[j] = kk[j] == kSent ? S(0) : sv[(kk[j] & 63u) * kQR];
+    T head = 0, cur = 0;
+    uint32_t ccol = 0, idx = first, zeros = 0;
+    bool seen = false;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        if (kk[j] == kSent) continue;
+        if ((starts >> j) & 1u) {
+            if (seen) {
+                const S out = L::done(cur);
+                zeros += Sem::is_zero(out) ? 1u : 0u;
+                emit(ccol, out, idx++);
+            }
+            cur = (T)v[j];
+            ccol = kk[j] >> 6;
+            seen = true;
+        } else if (seen) {
+            cur = quad_comb<Sem>(cur, (T)v[j]);
+        } else {
+            head = quad_comb<Sem>(head, (T)v[j]);
+        }
+    }
+    // X_q = head_q + (a start in lane q ? 0 : X_{q+1}): what lane q adds to a run from before it
+    T x = head;
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+        const T xn = quad_perm64<kQNext>(x);
+        x = (q < 3 && !seen) ? quad_comb<Sem>(head, xn) : head;
+    }
+    const T xn = quad_perm64<kQNext>(x);
+    if (seen) {
+        const S out = L::done(quad_comb<Sem>(cur, q < 3 ? xn : T(0)));
+        zeros += Sem::is_zero(out) ? 1u : 0u;
+        emit(ccol, out, idx);
+    }
+    return zeros;
+}
+
 template <typename Sem>
 __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned long long *status, uint32_t epoch,
                                                                unsigned long long *maxw) {
@@ -194,6 +290,14 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
     const S *bv = (const S *)p.b_val;
     const auto plus = [](uint32_t x, uint32_t y) { return x + y; };
     const auto mx = [](uint32_t x, uint32_t y) { return max(x, y); };
+    // diagnostic builds (-DSLAT_PHASES=1): s_memtime cycles per phase, summed over waves
+    PhaseClock pc{};
+    if constexpr (SLAT_PHASES) {
+        pc.t = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int i = 0; i < kPhaseSlots; ++i) pc.ph[i] = 0;
+        pc.ph[kPhaseSlots - 1] = 1;
+    }
 
     // this wave's rows [r0, r0 + nt): lanes < nt hold their bounds
     const uint64_t r0 = (uint64_t)blockIdx.x * kLaneRows + (uint64_t)wv * kQR;
@@ -212,6 +316,7 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
     }
     if (threadIdx.x == 0) *s_max = 0;
     __syncthreads();  // (the block's max row word is clear before any wave adds to it)
+    pc.mark(0);  // row bounds
 
     // 1-2. the rows' entries 64 at a time, then their products flattened into the slot table
     uint32_t rcarry = 0, fcarry = 0;  // row (+1) running into the pass, flat products so far
@@ -240,6 +345,7 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
         }
         const uint32_t incl = wave_incl_scan(bl, 0u, plus);
         const uint32_t off = fcarry + incl - bl, stot = readlane_u32(incl, kWave - 1);
+        pc.mark(1);  // A entries, B row bounds
         if (first && i < A1) rbase[rl] = off;  // the row's first entry
         if (i < A1 && bl) atomicAdd(&rcnt[rl], bl);
         eb[lane] = bs - off;  // product t of the entry: B index eb + t
@@ -286,10 +392,13 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
             wave_sync();
         }
         fcarry += stot;
+        pc.mark(2);  // products into the slot table
     }
 
-    // 3. each row's keys sorted by its quad (lane 4r + q: row r, elements q * NL ..), then written
-    //    back row-major; lane q = 0 of the quad reads its row's N sorted keys into registers
+    // 3. each row's keys sorted by its quad (lane 4r + q: row r, elements q * NL ..); integer rows
+    //    are counted and summed by the quad from there (quad_count / quad_combine), f64 rows are
+    //    written back row-major and lane q = 0 of the quad reads its row's N sorted keys (the fold)
+    constexpr bool kQuad = !std::is_same_v<S, double>;
     const uint32_t r = lane >> 2, q = lane & 3u;
     const uint32_t cnt = r < nt ? rcnt[r] : 0u;
     if (cnt > kLaneCap)  // the host runs the call through the pipeline instead
@@ -298,6 +407,7 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
     const uint32_t wmax = wave_max_u32(cn);
     uint32_t nz = 0, zeros = 0, roff = 0;  // (q = 0 lanes) distinct columns, zero sums, offset in the wave
     uint32_t k[kLaneCap];
+    uint32_t kq[kLaneCap / 4], qst = 0, qfirst = 0;  // (integer rows) the lane's sorted keys, starts, first output
     auto sort_and_count = [&](auto ntag) {
         constexpr int N = decltype(ntag)::value, NL = N / 4;
         uint32_t kk[kLaneCap / 4];
@@ -307,6 +417,14 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
             kk[j] = e < cn ? skey[e * kQR + r] : kSent;
         }
         quad_sort<NL>(kk, q);
+        if constexpr (kQuad) {
+            uint32_t tot = 0;
+            quad_count<NL>(kk, q, qst, qfirst, tot);
+#pragma unroll
+            for (int j = 0; j < (int)kLaneCap / 4; ++j) kq[j] = j < NL ? kk[j] : kSent;
+            nz = q == 0 ? tot : 0u;
+            return;
+        }
         wave_sync();
 #pragma unroll
         for (int j = 0; j < NL; ++j) skey[r * kLaneCap + q * NL + (uint32_t)j] = kk[j];
@@ -333,7 +451,9 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
     if (lane == 0) s_wsum[wv] = wsum;
     const uint32_t rmax = wave_max_u32(nz);
     if (lane == 0 && rmax) atomicMax(s_max, rmax);
+    pc.mark(3);  // sort, count
     __syncthreads();
+    pc.mark(4);  // block barrier
     // 4. the block's aggregate published first; u32 rows then stage their outputs in LDS at the
     //    block-local offset while the earlier blocks finish, and only the coalesced store waits for
     //    the offset (decoupled look-back over the earlier blocks' status words)
@@ -347,33 +467,37 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
     if (threadIdx.x == 0) {
         // the max row first, its result waited for: it is in place once a later block sees this
         // block's status, so the last block reads the final max after its look-back
-        pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | *s_max));
+        maxw_raise(maxw, epoch, *s_max);
         lookback_publish(status, blockIdx.x, epoch, agg);
     }
     const S *sv = sval + r;  // slot e of this lane's row at sv[e * kQR]
+    // (integer rows) the quad's outputs by every lane of it, at the row's offset q = 0 holds
+    const uint32_t roffq = kQuad ? quad_perm<kQFirst>(roff) : roff;
+    auto quad_all = [&](auto &&emit) {
+        if (wmax <= 16)
+            return quad_combine<Sem, 4>(kq, qst, qfirst, sv, q, emit);
+        else if (wmax <= 32)
+            return quad_combine<Sem, 8>(kq, qst, qfirst, sv, q, emit);
+        else
+            return quad_combine<Sem, 16>(kq, qst, qfirst, sv, q, emit);
+    };
     if constexpr (sizeof(S) == 4) {
-        if (q == 0 && nz) {
-            const uint32_t o0 = wbase + roff;
-            auto emit = [&](uint32_t col, S val, uint32_t j) {
-                stc[o0 + j] = col;
-                stv[o0 + j] = val;
-            };
-            if (wmax <= 16)
-                zeros = lane_combine<Sem, 16>(k, sv, emit);
-            else if (wmax <= 32)
-                zeros = lane_combine<Sem, 32>(k, sv, emit);
-            else
-                zeros = lane_combine<Sem, 64>(k, sv, emit);
-        }
+        const uint32_t o0 = wbase + roffq;
+        zeros = quad_all([&](uint32_t col, S val, uint32_t j) {
+            stc[o0 + j] = col;
+            stv[o0 + j] = val;
+        });
     }
+    pc.mark(5);  // publish, combine into staging
     __syncthreads();
+    pc.mark(6);  // block barrier
     if (wv == 0) {
         const unsigned long long excl = lookback_walk(status, blockIdx.x, epoch, agg);
+        const bool last = blockIdx.x == gridDim.x - 1;
+        const unsigned long long mxr = last ? maxw_read(maxw, epoch) : 0u;
         if (lane == 0) {
             *s_off = excl;
-            if (blockIdx.x == gridDim.x - 1) {
-                const unsigned long long mw = __hip_atomic_load(maxw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long mxr = (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull;
+            if (last) {
                 const unsigned long long o0 =
                     __hip_atomic_exchange(&p.host_out[0], excl + agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 const unsigned long long o1 =
@@ -383,6 +507,7 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
         }
     }
     __syncthreads();
+    pc.mark(7);  // look-back (wave 0), barrier
     const unsigned long long excl = *s_off;
     const uint64_t base = excl + wbase + roff;  // (q = 0 lanes) the row's first output
     if (q == 0 && r < nt) {
@@ -397,6 +522,14 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
             oc[u] = stc[u];
             ov[u] = stv[u];
         }
+    } else if constexpr (kQuad) {
+        const uint64_t bq = excl + wbase + roffq;
+        uint32_t *oc = p.c_col + bq;
+        S *ov = (S *)p.c_val + bq;
+        zeros = quad_all([&](uint32_t col, S val, uint32_t j) {
+            oc[j] = col;
+            ov[j] = val;
+        });
     } else if (q == 0 && nz) {
         uint32_t *oc = p.c_col + base;
         S *ov = (S *)p.c_val + base;
@@ -414,8 +547,20 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
     // zero sums (explicit zero inputs, f64 cancellation) stay in C for now: the row's non-zero count
     // goes to p.counts and the rows with zeros to host_out[2], and the host compacts (as after
     // k_numeric)
+    if constexpr (kQuad) {  // the row's zero sums from its quad's lanes, kept in lane q = 0
+        zeros += quad_perm<0xB1>(zeros);  // [1,0,3,2]
+        zeros += quad_perm<0x4E>(zeros);  // [2,3,0,1]
+        if (q != 0) zeros = 0;
+    }
     if (q == 0 && r < nt) p.counts[r0 + r] = nz - zeros;
     add_zero_rows(&p.host_out[2], wave_sum_u32(zeros ? 1u : 0u), true);
+    pc.mark(8);  // stores
+    if constexpr (SLAT_PHASES) {
+        if (lane == 0) {
+            unsigned long long *dst = p.shards + 512 + ((blockIdx.x * kLaneWaves + wv) % 64) * kPhaseSlots;
+            for (int i = 0; i < kPhaseSlots; ++i) atomicAdd(&dst[i], (unsigned long long)pc.ph[i]);
+        }
+    }
     signal_done(p);
 }
 

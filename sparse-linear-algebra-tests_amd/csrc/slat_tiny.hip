@@ -88,12 +88,12 @@ __global__ __launch_bounds__(kBlock) void k_tiny(Args p, unsigned long long *sta
         }
         // the max row first (its result waited for): it is in place once a later block sees this
         // block's status, so the last block reads the final max after its look-back
-        if (threadIdx.x == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | mx));
+        if (threadIdx.x == 0) maxw_raise(maxw, epoch, mx);
         const unsigned long long excl = lookback_prefix_wave(status, blockIdx.x, epoch, agg);
         if (threadIdx.x == 0) s_pre = excl;
-        if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) {
-            const unsigned long long mw = __hip_atomic_load(maxw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long mxr = (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull;
+        const bool last = blockIdx.x == gridDim.x - 1;
+        const unsigned long long mxr = last ? maxw_read(maxw, epoch) : 0u;
+        if (threadIdx.x == 0 && last) {
             // returned values: both words have landed before this block reports done (signal_done)
             const unsigned long long o0 =
                 __hip_atomic_exchange(&p.host_out[0], excl + agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

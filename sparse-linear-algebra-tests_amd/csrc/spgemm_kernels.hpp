@@ -198,6 +198,21 @@ __device__ __forceinline__ void signal_done(const Args &p) {
     }
 }
 
+// The call's max row count in the one-kernel paths (k_tiny, k_lane), two-level like the done count:
+// block b raises word b % 8 (kDoneStride apart) with an epoch-tagged atomicMax and waits for it, so
+// the max is in place before any later block can see this block's look-back status; the last block
+// takes the max over the eight words of this epoch after its walk. (One word took the launch's ~420
+// blocks' atomics in a row, ~15 ns each, all arriving after their sorts: the last blocks' look-back
+// publishes waited up to ~6 us behind them.)
+constexpr size_t kMaxwBytes = (size_t)kDoneStride * kDoneGroups * 8;
+__device__ __forceinline__ void maxw_raise(unsigned long long *maxw8, uint32_t epoch, uint32_t mx) {
+    const unsigned long long old =
+        atomicMax(&maxw8[(size_t)kDoneStride * (blockIdx.x % kDoneGroups)], ((unsigned long long)epoch << 32) | mx);
+    asm volatile("" ::"v"(old));  // wait for it
+}
+// (a whole wave) the max over the eight words raised in this epoch
+__device__ __forceinline__ uint32_t maxw_read(unsigned long long *maxw8, uint32_t epoch);
+
 // ------------------------------------------------------------------------------------------------
 // value semirings: S storage type, P cached product, V LDS accumulator
 // ------------------------------------------------------------------------------------------------
@@ -342,6 +357,15 @@ __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
 }
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     return ((uint64_t)readlane_u32((uint32_t)(v >> 32), l) << 32) | readlane_u32((uint32_t)v, l);
+}
+__device__ __forceinline__ uint32_t maxw_read(unsigned long long *maxw8, uint32_t epoch) {
+    uint32_t m = 0;
+    if (lane_id() < (int)kDoneGroups) {
+        const unsigned long long w =
+            __hip_atomic_load(&maxw8[(size_t)kDoneStride * lane_id()], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        m = (uint32_t)(w >> 32) == epoch ? (uint32_t)w : 0u;
+    }
+    return wave_max_u32(m);
 }
 
 // Work items handed out by a ticket counter instead of a fixed stride, so waves that drew cheap items
@@ -2879,7 +2903,6 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
     __shared__ uint32_t wmax[kScanThreads / kWave];
     const int t = threadIdx.x, lane = lane_id(), w = t / kWave;
     const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
-    auto ld = [](unsigned long long *x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     // (tile 0's last wave) k_build_ell's B-value partials, the first 8 per lane loaded now, so they
     // land under the tile's scan instead of after it (a chain of dependent loads at the end of the
     // kernel: 211 partials on the headline)
@@ -2933,17 +2956,16 @@ static __global__ __launch_bounds__(kScanThreads) void k_scan_rows(const uint64_
             for (int k = 0; k < kScanThreads / kWave; ++k) m = max(m, wmax[k]);
             // max row first (its result waited for), then the status: the max is in place once any
             // later tile sees this tile's status (bmax: the last tile has it from the producer's maxima)
-            if (!bmax && lane == 0) pin_u64(atomicMax(maxw, ((unsigned long long)epoch << 32) | m));
+            if (!bmax && lane == 0) maxw_raise(maxw, epoch, m);
             // the walk by the whole wave, 256 predecessors per round: a lane-0 walk was one dependent
             // load per predecessor still holding only its aggregate (one rank's eighth of C4, 62
             // tiles: 18.8 us for a 1 MB scan)
             const unsigned long long excl = lookback_prefix_wave(status, tile, epoch, agg);
             if (lane == 0) s_bcast[1] = excl;
+            const uint32_t mr = tile == ntiles - 1 ? (bmax ? m : maxw_read(maxw, epoch)) : 0u;
             if (lane == 0 && tile == ntiles - 1) {
                 if (n > 0) rp[0] = 0;
-                const unsigned long long mw = bmax ? 0ull : ld(maxw);
-                const unsigned long long out[2] = {excl + agg, bmax ? (unsigned long long)m
-                                                                    : (uint32_t)(mw >> 32) == epoch ? (mw & 0xFFFFFFFFull) : 0ull};
+                const unsigned long long out[2] = {excl + agg, (unsigned long long)mr};
                 for (int k = 0; k < 2; ++k)
                     __hip_atomic_store(&host_out[k], out[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
