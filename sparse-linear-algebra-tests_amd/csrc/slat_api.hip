@@ -778,9 +778,9 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     // 30^3 sweep's e/n-4 cell overflowed on every call and paid both paths, 95 -> 149 us)
     if (lane && (unsigned __int128)A->max_row_nnz * maxrow_b > slat_lane_cap())
         for (const auto &m : ctx->lane_miss)
-            if (m.kind == 0 && m.a_rp == A->row_ptr && m.a_col == A->col_idx && m.b_rp == B->row_ptr &&
-                m.b_col == B->col_idx && m.a_nnz == A->nnz && m.b_nnz == B->nnz && m.a_rows == A->n_rows &&
-                m.row_begin == row_begin && m.row_end == row_end)
+            if (m.a_rp == A->row_ptr && m.a_col == A->col_idx && m.b_rp == B->row_ptr && m.b_col == B->col_idx &&
+                m.a_nnz == A->nnz && m.b_nnz == B->nnz && m.a_rows == A->n_rows && m.row_begin == row_begin &&
+                m.row_end == row_end)
                 lane = false;
     static const bool kNoEll = slat_ab_knob("SLAT_NO_ELL") != nullptr;
     const bool ell = ell_fits(B, maxrow_b, vs) && !kNoEll && !tiny && !lane;
@@ -928,24 +928,6 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     const uint64_t maxrow_a = A->max_row_nnz;
     const uint64_t fat_min = slat_fat_min(!ell && (dt != SLAT_F64 || f64any));
     const bool fat = !kNoFat && !tiny && !lane && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= fat_min : maxrow_b > 32);
-    // wide products whose rows are all short (config C4, its row blocks): the whole call in one kernel
-    // (slat_short1p.hip) instead of symbolic, scan, numeric and the two listed-row launches. u32 with
-    // B's ELL image, no fat rows, A rows of <= 256 entries, packed sort keys ((3 << cb | column) << 9
-    // | slot below kSent). A row the tables cannot take sets the overflow word: the call reruns through
-    // the pipeline and the operands are remembered (kind 1)
-    static const bool kNo1p = slat_ab_knob("SLAT_NO_1P") != nullptr;
-    uint32_t cb1 = 1;
-    while (cb1 < 32 && ((ncols - 1) >> cb1)) ++cb1;
-    bool onep = !kNo1p && dt == SLAT_U32 && asym.wide && ell && !fat && !tiny && !lane && idx32 && wait_mode() == 0 &&
-                !ablate && !progress && !(flags & (SLAT_FLAG_STATS | SLAT_FLAG_TIMING | SLAT_FLAG_NO_TINY)) &&
-                A->max_row_nnz && A->max_row_nnz <= 256 && cb1 <= 21 &&
-                ((((3ull << cb1) | (ncols - 1)) << 9) | 511ull) < 0xFFFFFFFFull;
-    if (onep)
-        for (const auto &m : ctx->lane_miss)
-            if (m.kind == 1 && m.a_rp == A->row_ptr && m.a_col == A->col_idx && m.b_rp == B->row_ptr &&
-                m.b_col == B->col_idx && m.a_nnz == A->nnz && m.b_nnz == B->nnz && m.a_rows == A->n_rows &&
-                m.row_begin == row_begin && m.row_end == row_end)
-                onep = false;
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (bell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
@@ -1077,7 +1059,6 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     hipError_t e;
     const bool run_tiny = tiny && !exact;
     const bool run_lane = lane && !exact;
-    const bool run_1p = onep && !exact;
     if (run_tiny) {
         // the whole call in one kernel: a wave per row, every block resident (<= 1024 blocks of
         // <= 30 KB LDS), block offsets by look-back; it stores the completion word itself
@@ -1112,32 +1093,8 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         SLAT_HIPC(wait_stream(ctx, s, a.seq));
         if (ctx->h_out[3]) {
             ctx->lane_miss[ctx->lane_miss_next++ % 8] = {A->row_ptr, A->col_idx, B->row_ptr, B->col_idx, A->nnz,
-                                                         B->nnz,     A->n_rows,   row_begin, row_end,  0};
+                                                         B->nnz,     A->n_rows,   row_begin, row_end};
             // a row of more than slat_lane_cap() products: the call through the pipeline
-            (void)failc(SLAT_OK);
-            return rowblock_impl(ctx, A, row_begin, row_end, B, prep, C, flags | SLAT_FLAG_NO_TINY);
-        }
-    } else if (run_1p) {
-        // the whole call in one kernel, a tile of rows per wave, block offsets by look-back; a one-thread
-        // kernel after it stores the completion word (the grid has ~n / 8 blocks: a done count per
-        // block would queue that many device-scope atomics)
-        a.c_col = C->col_idx;
-        a.c_val = C->values;
-        a.cbits = cb1;
-        const uint64_t g = (n + slat_short1p_rows() - 1) / slat_short1p_rows();
-        if ((st = ensure_status(ctx, g, s))) return failc(st);
-        const uint32_t epoch = slat_next_scan_epoch(ctx, s);
-        if (bell)  // the B-value summary for the narrow batches (the pipeline's scan reduces it)
-            hipLaunchKernelGGL(k_reduce_bparts, dim3(1), dim3(kWave), 0, s, (const unsigned long long *)(ws + o_part),
-                               build_ell_blocks(B, a.ell_wq), ctx->d_vmax, a.epoch);
-        if (SLAT_PHASES) SLAT_HIPC(hipMemsetAsync(a.shards, 0, shards_b, s));
-        SLAT_HIPC(slat_launch_short1p(dim3((unsigned)g), s, a, ctx->d_status, epoch, ctx->d_maxw));
-        hc.mark(5);
-        hc.mark(6);
-        SLAT_HIPC(wait_stream(ctx, s, 0));
-        if (ctx->h_out[3]) {
-            ctx->lane_miss[ctx->lane_miss_next++ % 8] = {A->row_ptr, A->col_idx, B->row_ptr, B->col_idx, A->nnz,
-                                                         B->nnz,     A->n_rows,   row_begin, row_end,  1};
             (void)failc(SLAT_OK);
             return rowblock_impl(ctx, A, row_begin, row_end, B, prep, C, flags | SLAT_FLAG_NO_TINY);
         }
@@ -1371,7 +1328,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     S.nnz = nnz;
     S.flops = flops;
     S.capacity = C->capacity;
-    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u) | (run_lane ? 8u : 0u) | (run_1p ? 16u : 0u);
+    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u) | (run_lane ? 8u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;

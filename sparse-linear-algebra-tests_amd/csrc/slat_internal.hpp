@@ -56,11 +56,9 @@ struct slat_ctx {
     // products): the next call on the same triple goes to the pipeline directly instead of running
     // both. Keyed by both operands' arrays, sizes and the row range; an entry whose array the context
     // frees is dropped (slat_dev_free), so a new matrix at a recycled address starts clean
-    // (kind 0: the lane kernel; 1: the one-kernel wide product, slat_short1p.hip)
     struct LaneMiss {
         const void *a_rp, *a_col, *b_rp, *b_col;
         uint64_t a_nnz, b_nnz, a_rows, row_begin, row_end;
-        uint32_t kind;
     } lane_miss[8] = {};
     uint32_t lane_miss_next = 0;
     unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)

@@ -68,14 +68,6 @@ int slat_symbolic_listed_blocks_per_cu(bool idx32, bool ell, size_t lds);
 // rows of at most slat_lane_cap() products in one kernel, a row per lane (slat_lane.hip): n rows in
 // ceil(n / 64) one-wave blocks, status = look-back words (>= the block count), maxw = max-row word;
 // sets host_out[3] when a row has more products than the cap
-// wide products whose rows are all short (u32, B's ELL image) in one kernel (slat_short1p.hip):
-// slat_short1p_rows() rows per block, status = look-back words (>= the block count), maxw = max-row
-// words; sets host_out[3] when a row does not fit the tables
-uint32_t slat_short1p_rows();  // rows per block
-size_t slat_short1p_lds();
-hipError_t slat_launch_short1p(dim3 grid, hipStream_t s, const slat::Args &a, unsigned long long *status,
-                               uint32_t epoch, unsigned long long *maxw);
-
 uint32_t slat_lane_cap();
 uint32_t slat_lane_rows();  // rows per block
 hipError_t slat_launch_lane(int sem, dim3 grid, hipStream_t s, const slat::Args &a, unsigned long long *status,

@@ -111,8 +111,7 @@ struct Args {
     uint32_t ablate; // experiments only (SLAT_ABLATE): 1 = symbolic skips its LDS bitmap
     const uint32_t *ell_col;  // [n_B][ell_wq*4] columns, kSent padded
     const void *ell_val;      // [n_B][ell_wq*4] values
-    const uint8_t *ell_ng;    // [n_B] groups of 4 holding real entries, ceil(len / 4), in bits 0-3; the
-                              // last group's padding 4 * groups - len in bits 4-5
+    const uint8_t *ell_ng;    // [n_B] groups of 4 holding real entries: ceil(len / 4)
     unsigned long long *b_vmax;  // B-value summary from k_build_ell (u32 only; else null): [kVMaxWord]
                                  // (epoch << 32) | max, [kVMinInvWord] (epoch << 32) | ~min
     uint32_t epoch;
@@ -537,8 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_build_ell(const uint64_t *rp, const 
         const uint32_t k = g / wq;
         const uint32_t t = g - k * wq;
         const uint64_t s0 = rp[k], len = rp[k + 1] - s0;
-        // groups of 4 in the low nibble, the last group's padding (4 * groups - len) above it
-        if (t == 0) eng[k] = (uint8_t)(((len + 3) / 4) | ((((len + 3) / 4) * 4 - len) << 4));
+        if (t == 0) eng[k] = (uint8_t)((len + 3) / 4);
         uint32_t c[4];
         S v[4];
 #pragma unroll
@@ -696,7 +694,7 @@ __device__ __forceinline__ uint32_t short_brow(const Args &p, uint32_t &k) {
         k = (uint32_t)r0;
         return (uint32_t)min<uint64_t>(r1 - r0, 1u << 30);
     } else {
-        return p.ell_ng[k] & 15u;
+        return p.ell_ng[k];
     }
 }
 template <bool CSR>
@@ -1252,7 +1250,7 @@ struct RowWalker {
         uint32_t mx = 0;
         sfor<kRegQ>([&](auto Q) {
             constexpr int q = Q;
-            ngq[q] = kq[q] != kSent ? p.ell_ng[kq[q]] & 15u : 0u;
+            ngq[q] = kq[q] != kSent ? p.ell_ng[kq[q]] : 0u;
             mx = max(mx, ngq[q]);
         });
         mx = wave_max_u32(mx);
