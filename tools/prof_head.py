@@ -15,8 +15,8 @@ for _ in range(20):
     P.matmul(A).nnz()
 ctx.sync()
 t0 = time.perf_counter()
-for _ in range(40):
+for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 40):
     C = P.matmul(A)
     C.nnz()
     del C
-print(f"headline: {(time.perf_counter() - t0) / 40 * 1e3:.4f} ms per call", flush=True)
+print(f"headline: {(time.perf_counter() - t0) / (int(sys.argv[1]) if len(sys.argv) > 1 else 40) * 1e3:.4f} ms per call", flush=True)
