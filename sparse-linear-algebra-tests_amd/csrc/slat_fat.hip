@@ -457,6 +457,22 @@ __global__ __launch_bounds__(kFB) void k_fr_symbolic(FatArgs f) {
     }
 }
 
+// f64 in the reference's order: acc[o] += p. SLAT_FOLD_ATOMIC (default): one LDS atomic add
+// (ds_add_f64: an IEEE double add, round to nearest even, as v_add_f64). A wave's LDS instructions
+// execute in issue order, so the adds of successive A entries to one column still land in A order —
+// the left fold bit for bit — with no wait between entries; otherwise a read, an add and a write, then
+// an LDS fence before the next entry (same columns are possible). A wave owns its column slice, so no
+// other wave touches these slots.
+__device__ __forceinline__ void fold_add(double *acc, uint32_t o, double p) {
+    if constexpr (SLAT_FOLD_ATOMIC)
+        (void)__hip_atomic_fetch_add(&acc[o], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+        acc[o] = __dadd_rn(acc[o], p);
+}
+__device__ __forceinline__ void fold_sync() {
+    if constexpr (!SLAT_FOLD_ATOMIC) wave_sync();
+}
+
 // The chunk's products into the dense accumulator. Integer semirings / f64 any order: LDS atomics,
 // lanes over A entries. f64 in the reference's order: wave w owns columns [c0 + w*span, ...) and
 // walks the A entries in order, lanes over one B row (distinct columns): one writer per column.
@@ -575,18 +591,18 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                     if (s != e) {  // wave-uniform
                         if (s + (I)lane < e) {
                             const uint32_t o = q.c[U] - c0;
-                            acc[o] = __dadd_rn(acc[o], __dmul_rn(q.a[U], q.v[U]));
+                            fold_add(acc, o, __dmul_rn(q.a[U], q.v[U]));
                             atomicOr(&bits[o >> 5], 1u << (o & 31));
                         }
-                        wave_sync();  // this entry's adds land before the next entry's (same columns)
+                        fold_sync();  // this entry's adds land before the next entry's (same columns)
                         for (I j0 = s + (I)kWave; j0 < e; j0 += (I)kWave) {  // a part longer than a wave
                             const I j = j0 + (I)lane;
                             if (j < e) {
                                 const uint32_t o = p.b_col[j] - c0;
-                                acc[o] = __dadd_rn(acc[o], __dmul_rn(q.a[U], bv[j]));
+                                fold_add(acc, o, __dmul_rn(q.a[U], bv[j]));
                                 atomicOr(&bits[o >> 5], 1u << (o & 31));
                             }
-                            wave_sync();
+                            fold_sync();
                         }
                     }
                 });
@@ -640,10 +656,10 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
                 b_range<I>(p.b_col, s0, e0, lo, hi, s, e);
                 for (I j = s + (I)lane; j < e; j += (I)kWave) {
                     const uint32_t o = p.b_col[j] - c0;
-                    acc[o] = __dadd_rn(acc[o], __dmul_rn(at, bv[j]));
+                    fold_add(acc, o, __dmul_rn(at, bv[j]));
                     atomicOr(&bits[o >> 5], 1u << (o & 31));
                 }
-                wave_sync();  // this entry's adds land before the next entry's (same columns)
+                fold_sync();  // this entry's adds land before the next entry's (same columns)
             }
         }
     }

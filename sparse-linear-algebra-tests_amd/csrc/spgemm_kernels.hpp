@@ -51,6 +51,9 @@ constexpr int kShardStride = 4;  // [0] total nnz (shard 0), [1] max row nnz, [2
 #ifndef SLAT_PHASES
 #define SLAT_PHASES 0  // diagnostic builds: per-phase s_memtime cycles of k_numeric
 #endif
+#ifndef SLAT_FOLD_ATOMIC
+#define SLAT_FOLD_ATOMIC 1  // f64 in the fold order: slot adds as in-order LDS atomics (variant builds: 0)
+#endif
 #ifndef SLAT_SHORT_PACK
 #define SLAT_SHORT_PACK 1  // k_numeric_short: payload-free emit sort of (key << 9 | slot) when it fits 32 bits
 #endif
@@ -267,8 +270,17 @@ struct SemF64 {
     static constexpr bool kOrdered = true;
     static constexpr bool kNarrowable = false;
     __device__ static __forceinline__ P prod(S a, S b) { return __dmul_rn(a, b); }
+    // no FMA contraction: Rust's a*b then +. One LDS atomic add (ds_add_f64, an IEEE double add,
+    // round to nearest even) instead of a read, an add and a write: the ordered walks give a row's
+    // slots to one wave and add its A entries in order, and a wave's LDS instructions execute in
+    // issue order, so the adds to one slot land in A order (the left fold) without each entry waiting
+    // for the previous one's write (SLAT_FOLD_ATOMIC=0: the read-add-write)
     __device__ static __forceinline__ void acc(V *vals, uint32_t r, P p) {
-        vals[r] = __dadd_rn(vals[r], p);  // no FMA contraction: Rust's a*b then +
+#if SLAT_FOLD_ATOMIC
+        (void)__hip_atomic_fetch_add(&vals[r], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+        vals[r] = __dadd_rn(vals[r], p);
+#endif
     }
     __device__ static __forceinline__ S finish(const V *vals, uint32_t t) { return vals[t]; }
     __device__ static __forceinline__ bool is_zero(S v) { return v == 0.0; }
