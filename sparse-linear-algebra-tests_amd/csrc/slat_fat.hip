@@ -562,44 +562,48 @@ __device__ __forceinline__ void fr_accumulate(const FatArgs &f, I a0, I a1, uint
             // entries' B loads are issued before this kFD's products are added (adds stay in entry
             // order; only the loads move ahead)
             constexpr int kFD = SLAT_FOLD_DEPTH;
+            // an entry ahead holds only its lane in the group: its bounds and A value are read again
+            // from the group's registers when it is applied (holding them took 16 x 2 x 4 SGPRs,
+            // 192 spilled: C5 2^18 fold 77.8 -> 73.2 ms, profiles/r05_fold_lane_ab18.txt)
             struct Ent {
                 uint32_t c[kFD];
-                S v[kFD], a[kFD];
-                I s[kFD], e[kFD];
+                S v[kFD];
+                int t[kFD];
             };
             auto fetch = [&](Ent &q) {
                 sfor<kFD>([&](auto U) {
-                    q.s[U] = q.e[U] = 0;
-                    q.a[U] = q.v[U] = S(0);
+                    q.t[U] = -1;
+                    q.v[U] = S(0);
                     q.c[U] = 0;
                     if (m) {
                         const int t = (int)__builtin_ctzll(m);
                         m &= m - 1;
-                        q.s[U] = (I)readlane_u64((uint64_t)bs_now, t);
-                        q.e[U] = (I)readlane_u64((uint64_t)be_now, t);
-                        q.a[U] = readlane_val(a_now, t);
-                        if (q.s[U] + (I)lane < q.e[U]) {
-                            q.c[U] = p.b_col[q.s[U] + (I)lane];
-                            q.v[U] = bv[q.s[U] + (I)lane];
+                        q.t[U] = t;
+                        const I s0 = (I)readlane_u64((uint64_t)bs_now, t), e0 = (I)readlane_u64((uint64_t)be_now, t);
+                        if (s0 + (I)lane < e0) {
+                            q.c[U] = p.b_col[s0 + (I)lane];
+                            q.v[U] = bv[s0 + (I)lane];
                         }
                     }
                 });
             };
             auto apply = [&](const Ent &q) {
                 sfor<kFD>([&](auto U) {
-                    const I s = q.s[U], e = q.e[U];
-                    if (s != e) {  // wave-uniform
+                    const int t = q.t[U];
+                    if (t >= 0) {  // wave-uniform
+                        const I s = (I)readlane_u64((uint64_t)bs_now, t), e = (I)readlane_u64((uint64_t)be_now, t);
+                        const S a = readlane_val(a_now, t);
                         if (s + (I)lane < e) {
                             const uint32_t o = q.c[U] - c0;
-                            fold_add(acc, o, __dmul_rn(q.a[U], q.v[U]));
+                            fold_add(acc, o, __dmul_rn(a, q.v[U]));
                             atomicOr(&bits[o >> 5], 1u << (o & 31));
                         }
-                        fold_sync();  // this entry's adds land before the next entry's (same columns)
-                        for (I j0 = s + (I)kWave; j0 < e; j0 += (I)kWave) {  // a part longer than a wave
+                        fold_sync();
+                        for (I j0 = s + (I)kWave; j0 < e; j0 += (I)kWave) {
                             const I j = j0 + (I)lane;
                             if (j < e) {
                                 const uint32_t o = p.b_col[j] - c0;
-                                fold_add(acc, o, __dmul_rn(q.a[U], bv[j]));
+                                fold_add(acc, o, __dmul_rn(a, bv[j]));
                                 atomicOr(&bits[o >> 5], 1u << (o & 31));
                             }
                             fold_sync();
