@@ -1,0 +1,16 @@
+#!/bin/bash
+# round-5 closing check on one box: the GPU suite, smoke and the default bench line on the final tree, then
+# the heavy legs once (2^16 and 2^18)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/${1:-r05final2}; mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
+head -c 300 $OUT/bench.json; echo
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { tail $OUT/smoke.txt; exit 1; }
+cat $OUT/smoke.txt
+timeout -k 10 300 python3 tools/ab_heavy.py --child --legs rg,c5any,c5ord,chain > $OUT/heavy16.txt 2>&1 || { tail $OUT/heavy16.txt; exit 1; }
+tail -1 $OUT/heavy16.txt | cut -c1-600
+timeout -k 10 400 python3 tools/ab_heavy.py --child --big --legs c5big_any,c5big_ord > $OUT/heavy18.txt 2>&1 || { tail $OUT/heavy18.txt; exit 1; }
+tail -1 $OUT/heavy18.txt | cut -c1-600
