@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-5 last check on one box after the final rebuild: the GPU suite, smoke and the default bench line
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/${1:-r05final4}; mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.txt 2>&1 || { tail $OUT/smoke.txt; exit 1; }
+cat $OUT/smoke.txt
+timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 1; }
+head -c 300 $OUT/bench.json; echo
