@@ -464,7 +464,10 @@ __device__ __forceinline__ uint32_t sat32(S v) {
 // columns), 64 A entries' row pointers prefetched at a time. The first 64 elements of the B rows
 // of kOrdAhead consecutive entries are loaded before any of them is visited, so the visits (in A
 // order: the left fold of linalg/src/csr.rs:325-337) do not wait on one load chain per entry.
-constexpr int kOrdAhead = 8;
+#ifndef SLAT_ORD_AHEAD
+#define SLAT_ORD_AHEAD 8  // (variant builds: 4, 16)
+#endif
+constexpr int kOrdAhead = SLAT_ORD_AHEAD;
 template <typename I, typename S, typename F>
 __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&visit) {
     const int lane = lane_id();
