@@ -119,7 +119,8 @@ typedef struct {
     double numeric_ms;
     double compact_ms;
     double total_ms;       /* first event to last event on the stream */
-    uint32_t mode;         /* bits: 1 = 32-bit offsets, 2 = B's ELL image, 4 = the one-kernel small path */
+    uint32_t mode;         /* bits: 1 = 32-bit offsets, 2 = B's ELL image, 4 = the one-kernel small path,
+                              8 = the lane kernel, 16 = the stored-bitmap numeric pass (MODE 4) */
     uint32_t window_words; /* LDS bitmap words per window */
     uint32_t exact_alloc;  /* 1 if the mid-call-sync path was taken */
     uint32_t dropped_rows; /* rows that lost explicit zeros in the numeric pass */

@@ -489,7 +489,12 @@ slat_status slat_launch_scan(slat_ctx *ctx, const uint64_t *counts, uint64_t n, 
     slat_status st;
     if ((st = ensure_status(ctx, tiles, s))) return st;
     const uint32_t epoch = slat_next_scan_epoch(ctx, s);
-    // at most one block per CU, each taking its tiles in order (k_scan_rows)
+    // At most one block per CU, each taking its tiles in order (k_scan_rows: block b walks tiles b,
+    // b + G, ...). Block 0's second tile looks back on tile G - 1, so when tiles > G forward progress
+    // assumes all G blocks are resident at once. G <= the CU count, and one CU holds several of these
+    // blocks (256 threads, a few hundred bytes of LDS), so they co-reside unless another process
+    // holds every CU for the whole kernel; two ranks sharing one GPU (tests/test_dist_hip_gpu.py)
+    // time-slice, and their kernels retire. Earlier tiles' blocks never wait on later ones.
     const uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)ctx->cu_count);
     hipLaunchKernelGGL(k_scan_rows, dim3((unsigned)grid), dim3(kScanThreads), 0, s, counts, n, rp, ctx->d_status, epoch,
                        ctx->d_maxw, ctx->h_out_dev, bpart, nbpart, ctx->d_vmax, vepoch, bmax, nbmax, zero_word);
@@ -623,6 +628,7 @@ extern "C" slat_status slat_spgemm_rowblock_prepared(slat_ctx *ctx, const slat_c
                                                      uint64_t row_end, const slat_bprep *B, slat_csr *C, uint32_t flags) {
     if (!ctx || !B) return SLAT_EINVAL;
     if (B->device != ctx->device) return fail(ctx, SLAT_EINVAL, "prepared B belongs to another device");
+    if (B->owner != ctx) return fail(ctx, SLAT_EINVAL, "prepared B belongs to another context");
     return rowblock_impl(ctx, A, row_begin, row_end, &B->b, B, C, flags);
 }
 
@@ -903,7 +909,11 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         const uint64_t over = mode == 3 ? kNumOver : 1;
         return dim3((unsigned)std::max<uint64_t>(1, std::min(row_blocks, (uint64_t)ctx->cu_count * nbpc * over)));
     };
-    const dim3 grid = num_grid(hash ? 2 : 0, num_lds);
+    // the single-window numeric pass over stored bitmaps with B's ELL image: MODE 4 (spgemm_stored.hpp)
+    // for the semirings that add in any order (SLAT_NO_STORED_MODE: the generic MODE 0, A/B)
+    static const bool kNoStored = slat_ab_knob("SLAT_NO_STORED_MODE") != nullptr;
+    const int win_mode = hash ? 2 : (sbm && ell && !ablate && (dt != SLAT_F64 || f64any) && !kNoStored) ? 4 : 0;
+    const dim3 grid = num_grid(win_mode, num_lds);
     const dim3 hash_grid = hash ? num_grid(hash_mode, hash_lds) : dim3(1);
     const bool progress = g_progress.load(std::memory_order_relaxed) != 0;
     const bool timing = (flags & SLAT_FLAG_TIMING) || progress;
@@ -1192,7 +1202,10 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         // single-window launch without fat rows: symbolic leaves per-block max row counts for the
         // scan's last tile (<= 16 per scan thread)
         if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
-        SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
+        if (win_mode == 4)  // the stored-bitmap pair: symbolic MODE 4 (spgemm_stored.hpp)
+            SLAT_HIPC(slat_launch_symbolic(4, idx32, ell, sym_grid, (size_t)wpb * sym_stored_words(asym.ww) * 4, s, asym));
+        else
+            SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
     }
     hc.mark(5);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
@@ -1218,7 +1231,6 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     }
     a.c_col = C->col_idx;
     a.c_val = C->values;
-    const int win_mode = hash ? 2 : 0;  // numeric instance of the window rows
     auto launch_num = [&](const Args &x) { return slat_launch_numeric(sem, win_mode, idx32, ell, grid, num_lds, s, x); };
     if (ablate & ~7u) {
         // experiments only: an ablated numeric pass (writes stay inside C's row slices), timed;
@@ -1328,7 +1340,8 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     S.nnz = nnz;
     S.flops = flops;
     S.capacity = C->capacity;
-    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u) | (run_lane ? 8u : 0u);
+    S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u) | (run_lane ? 8u : 0u) |
+             (!run_tiny && !run_lane && win_mode == 4 ? 16u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;
@@ -1398,6 +1411,7 @@ extern "C" slat_status slat_bprep_create(slat_ctx *ctx, const slat_csr_view *B, 
     slat_bprep *p = new slat_bprep();
     p->b = *B;
     p->device = ctx->device;
+    p->owner = ctx;
     uint64_t mr = B->max_row_nnz;
     if (mr == 0 && B->n_rows && (st = slat_csr_max_row_nnz(ctx, B, &mr))) {
         delete p;

@@ -471,6 +471,7 @@ __device__ __forceinline__ void fold_add(double *acc, uint32_t o, double p) {
 }
 __device__ __forceinline__ void fold_sync() {
     if constexpr (!SLAT_FOLD_ATOMIC) wave_sync();
+    fold_order_point();  // the atomic adds: issue order made explicit to the compiler
 }
 
 // The chunk's products into the dense accumulator. Integer semirings / f64 any order: LDS atomics,

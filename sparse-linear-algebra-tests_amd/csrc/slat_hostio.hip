@@ -153,14 +153,20 @@ int hostio_mode() {
     return m;
 }
 
-bool is_pinned(const void *p) {
+// what a "host" segment's memory really is: pageable (0), page-locked host memory from hipHostMalloc
+// or hipHostRegister (1), or device / managed memory the runtime knows (2: copied with
+// hipMemcpyDefault, which reads the direction from the pointers, never through the staging ring)
+int mem_kind(const void *p) {
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();
-        return false;
+        return 0;
     }
-    return at.type == hipMemoryTypeHost || at.type == hipMemoryTypeManaged || at.type == hipMemoryTypeDevice;
+    if (at.type == hipMemoryTypeHost) return 1;
+    if (at.type == hipMemoryTypeManaged || at.type == hipMemoryTypeDevice) return 2;
+    return 0;
 }
+bool is_pinned(const void *p) { return mem_kind(p) != 0; }
 
 }  // namespace
 
@@ -210,9 +216,10 @@ void plan(const slat_hostseg *segs, int n, bool to_dev, hipStream_t s, std::vect
     for (int i = 0; i < n; ++i) {
         const slat_hostseg &g = segs[i];
         if (!g.bytes) continue;
-        if (is_pinned(g.host)) {
-            const hipError_t e = to_dev ? hipMemcpyAsync(g.dev, g.host, g.bytes, hipMemcpyHostToDevice, s)
-                                        : hipMemcpyAsync(g.host, g.dev, g.bytes, hipMemcpyDeviceToHost, s);
+        if (const int kind = mem_kind(g.host)) {
+            const hipMemcpyKind mk = kind == 2 ? hipMemcpyDefault : to_dev ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+            const hipError_t e = to_dev ? hipMemcpyAsync(g.dev, g.host, g.bytes, mk, s)
+                                        : hipMemcpyAsync(g.host, g.dev, g.bytes, mk, s);
             if (e != hipSuccess) err = e;
             continue;
         }

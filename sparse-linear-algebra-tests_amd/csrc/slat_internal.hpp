@@ -98,6 +98,7 @@ struct slat_bprep {
     unsigned long long *vmax = nullptr;
     uint32_t epoch = 0;
     int device = 0;
+    const slat_ctx *owner = nullptr;  // the context whose pool and stream hold the image
 };
 
 #define SLAT_HIP(ctx, expr)                                                                        \

@@ -284,8 +284,10 @@ __global__ __launch_bounds__(kLaneWaves * kWave) void k_lane(Args p, unsigned lo
     uint32_t *stc = (uint32_t *)blk;                          // (u32 values) staged columns
     S *stv = (S *)(blk + (size_t)kLaneCap * kLaneRows * 4);   // (u32 values) staged values
     uint32_t *s_wsum = (uint32_t *)(blk + (sizeof(S) == 4 ? (size_t)kLaneCap * kLaneRows * 8 : 0));
-    uint32_t *s_max = s_wsum + kLaneWaves;
-    unsigned long long *s_off = (unsigned long long *)(s_max + 4);
+    // the 32-byte tail of lane_lds(): wave sums at bytes 0-15, the max row at 16, the offset at 24-31
+    static_assert(kLaneWaves * 4 <= 16, "wave sums fit the tail's first 16 bytes");
+    uint32_t *s_max = s_wsum + 4;
+    unsigned long long *s_off = (unsigned long long *)(s_wsum + 6);
     const S *av = (const S *)p.a_val;
     const S *bv = (const S *)p.b_val;
     const auto plus = [](uint32_t x, uint32_t y) { return x + y; };

@@ -14,7 +14,8 @@ struct Args;
 enum { kSemU32 = 0, kSemSat64 = 1, kSemF64 = 2, kSemF64Any = 3, kSemCount = 4 };
 
 // numeric launch modes: 0 every row by bitmap windows; 1 one row per LDS hash table; 2 the listed
-// (window-category) rows of a wide launch; 3 batched short rows (integer semirings, ELL B)
+// (window-category) rows of a wide launch; 3 batched short rows (integer semirings, ELL B); 4 every row
+// of a single-window launch with stored bitmaps and B's ELL image (unordered semirings)
 template <int SEM>
 hipError_t slat_launch_numeric_t(int mode, bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s,
                                  const slat::Args &a);
@@ -49,7 +50,8 @@ static inline int slat_numeric_blocks_per_cu(int sem, int mode, bool idx32, bool
     }
 }
 
-// symbolic: mode 0 every row by windows, 1 one row per hash table, 2 the listed / window rows
+// symbolic: mode 0 every row by windows, 1 one row per hash table, 2 the listed / window rows, 4 every
+// row of a single-window launch that stores its bitmaps, B's ELL image (lds: sym_stored_words per wave)
 hipError_t slat_launch_symbolic(int mode, bool idx32, bool ell, dim3 grid, size_t lds, hipStream_t s,
                                 const slat::Args &a);
 // the whole product of a small call in one kernel (slat_tiny.hip): status / epoch: the look-back

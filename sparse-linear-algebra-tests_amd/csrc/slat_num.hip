@@ -36,6 +36,12 @@ hipError_t with_instance(int mode, bool idx32, bool ell, F &&f) {
     if (mode == 1)
         return idx32 ? (ell ? f(k_numeric<Sem, uint32_t, true, 1>) : f(k_numeric<Sem, uint32_t, false, 1>))
                      : (ell ? f(k_numeric<Sem, uint64_t, true, 1>) : f(k_numeric<Sem, uint64_t, false, 1>));
+    if (mode == 4) {  // single-window launches with stored bitmaps and B's ELL image (unordered semirings)
+        if constexpr (!Sem::kOrdered)
+            return idx32 ? f(k_numeric<Sem, uint32_t, true, 4>) : f(k_numeric<Sem, uint64_t, true, 4>);
+        else
+            return hipErrorInvalidValue;
+    }
     if (mode == 2)
         return idx32 ? (ell ? f(k_numeric<Sem, uint32_t, true, 2>) : f(k_numeric<Sem, uint32_t, false, 2>))
                      : (ell ? f(k_numeric<Sem, uint64_t, true, 2>) : f(k_numeric<Sem, uint64_t, false, 2>));
@@ -56,8 +62,8 @@ hipError_t slat_launch_numeric_t<SLAT_SEM>(int mode, bool idx32, bool ell, dim3 
 template <>
 int slat_numeric_blocks_per_cu_t<SLAT_SEM>(int mode, bool idx32, bool ell, size_t lds) {
     // cached per (instance, LDS size): the query costs microseconds of host time per call
-    static thread_local int cache_nb[16] = {};
-    static thread_local size_t cache_lds[16] = {};
+    static thread_local int cache_nb[32] = {};
+    static thread_local size_t cache_lds[32] = {};
     const int ci = (idx32 ? 1 : 0) | (ell ? 2 : 0) | (mode << 2);
     if (cache_lds[ci] == lds && cache_nb[ci] > 0) return cache_nb[ci];
     int nb = 0;

@@ -15,6 +15,8 @@ hipError_t slat_launch_symbolic(int mode, bool idx32, bool ell, dim3 grid, size_
     if (mode == 1)
         return idx32 ? (ell ? go(k_symbolic<uint32_t, true, 1>) : go(k_symbolic<uint32_t, false, 1>))
                      : (ell ? go(k_symbolic<uint64_t, true, 1>) : go(k_symbolic<uint64_t, false, 1>));
+    if (mode == 4)  // single-window launches with stored bitmaps and B's ELL image (spgemm_stored.hpp)
+        return ell ? (idx32 ? go(k_symbolic<uint32_t, true, 4>) : go(k_symbolic<uint64_t, true, 4>)) : hipErrorInvalidValue;
     if (mode == 2)
         return idx32 ? (ell ? go(k_symbolic<uint32_t, true, 2>) : go(k_symbolic<uint32_t, false, 2>))
                      : (ell ? go(k_symbolic<uint64_t, true, 2>) : go(k_symbolic<uint64_t, false, 2>));

@@ -464,10 +464,14 @@ __device__ __forceinline__ uint32_t sat32(S v) {
 // columns), 64 A entries' row pointers prefetched at a time. The first 64 elements of the B rows
 // of kOrdAhead consecutive entries are loaded before any of them is visited, so the visits (in A
 // order: the left fold of linalg/src/csr.rs:325-337) do not wait on one load chain per entry.
-#ifndef SLAT_ORD_AHEAD
-#define SLAT_ORD_AHEAD 8  // (variant builds: 4, 16)
-#endif
-constexpr int kOrdAhead = SLAT_ORD_AHEAD;
+// (4 and 16 measured within 1 % of 8 on C5 2^18, profiles/r05_ord_ahead_ab18.txt)
+constexpr int kOrdAhead = 8;
+// between two A entries of an ordered walk: a compiler-only barrier, so the relaxed LDS atomic adds
+// of one entry are issued before the next entry's (a wave's LDS instructions then execute in issue
+// order: the left fold). No hardware wait.
+__device__ __forceinline__ void fold_order_point() {
+    if constexpr (SLAT_FOLD_ATOMIC) asm volatile("" ::: "memory");
+}
 template <typename I, typename S, typename F>
 __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&visit) {
     const int lane = lane_id();
@@ -513,6 +517,7 @@ __device__ __forceinline__ void traverse_ordered(const Args &p, I a0, I a1, F &&
                     const S a = readlane_val(av, t);
                     if (q.c[G] != kSent) visit(q.c[G], a, q.v[G]);
                     for (I jdx = s + (I)kWave + (I)lane; jdx < e; jdx += (I)kWave) visit(p.b_col[jdx], a, bv_[jdx]);
+                    fold_order_point();
                 }
             });
         };
@@ -1635,6 +1640,10 @@ __device__ __forceinline__ uint64_t sym_row(const Args &p, uint64_t row, bool li
     return cnt;
 }
 
+}  // namespace slat
+#include "spgemm_stored.hpp"
+namespace slat {
+
 // variant builds: -DSLAT_SYM_WPE=w caps k_symbolic's registers for w waves per SIMD (0: no cap)
 #ifndef SLAT_SYM_WPE
 #define SLAT_SYM_WPE 0
@@ -1650,7 +1659,8 @@ void k_symbolic(Args p) {
     const int lane = lane_id();
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
     // per-wave words: the window bitmap, or (MODE 1) the hash keys
-    const uint32_t region_w = MODE == 1 ? kSymHashT : p.ww;
+    // (MODE 4 lays its regions out itself: sym_stored_words)
+    const uint32_t region_w = MODE == 1 ? kSymHashT : MODE == 4 ? 0u : p.ww;
     uint32_t *L0 = smem + (size_t)wv * region_w;
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) p.c_rp[0] = 0;
@@ -1688,6 +1698,9 @@ void k_symbolic(Args p) {
         if constexpr (kPre)
             if (r < nit && lane < 2) pre = p.a_rp[r + lane];
     };
+    if constexpr (MODE == 4) {
+        symbolic_rows_stored<I>(p, smem, wv, (uint64_t)blockIdx.x * kWpb + wv, stride, mx, flops);
+    } else {
     prefetch((uint64_t)blockIdx.x * kWpb + wv);
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
         if (dyn) pend = tq.issue();
@@ -1703,6 +1716,7 @@ void k_symbolic(Args p) {
         if (cnt == kNoRow) continue;
         if (lane == 0) p.counts[row] = cnt;
         mx = max(mx, cnt);
+    }
     }
     if (p.stats && lane == 0 && flops)
         atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
@@ -2123,12 +2137,16 @@ __device__ __forceinline__ void numeric_rows(const Args &p, uint8_t *smem8, int 
     add_zero_rows(&p.host_out[2], zrows, p.seq != 0);
 }
 
+// MODE 4: single-window launches with stored bitmaps and B's ELL image (spgemm_stored.hpp)
 template <typename Sem, typename I, bool ELL, int MODE = 0>
 __global__ __launch_bounds__(kBlock) SLAT_NUM_ATTR void k_numeric(Args p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem8[];
     constexpr int kWpb = kBlock / kWave;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // wave-uniform: row math in SGPRs
-    numeric_rows<Sem, I, ELL, MODE>(p, smem8, wv, (uint64_t)blockIdx.x * kWpb + wv, (uint64_t)gridDim.x * kWpb);
+    if constexpr (MODE == 4)
+        numeric_rows_stored<Sem, I>(p, smem8, wv, (uint64_t)blockIdx.x * kWpb + wv, (uint64_t)gridDim.x * kWpb);
+    else
+        numeric_rows<Sem, I, ELL, MODE>(p, smem8, wv, (uint64_t)blockIdx.x * kWpb + wv, (uint64_t)gridDim.x * kWpb);
     signal_done(p);
 }
 

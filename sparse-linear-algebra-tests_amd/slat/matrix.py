@@ -569,6 +569,10 @@ class DeviceCsr:
         if isinstance(other, PreparedB):
             if other.dtype != self.DTYPE:
                 raise TypeError("operands must have the same value type")
+            if other._ctx is not self._ctx:
+                # the handle's ELL image lives in its own context's pool and is released on that
+                # context's stream, which has no ordering against this one
+                raise ValueError("a PreparedB must be used with the context that prepared it")
             L.check(L.lib().slat_spgemm_rowblock_prepared(self._ctx.ptr, C.byref(a), row_begin, row_end, other.ptr,
                                                           C.byref(out), flags), self._ctx.ptr)
         else:
