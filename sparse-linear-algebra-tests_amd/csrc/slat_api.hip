@@ -259,8 +259,9 @@ void slat_dev_free(slat_ctx *ctx, void *p, hipStream_t s) {
     if (it == ctx->live.end()) return;  // not ours (or freed already)
     slat_ctx::Block b = it->second;
     ctx->live.erase(it);
-    for (auto &m : ctx->lane_miss)
-        if (m.a_rp == p || m.a_col == p || m.b_rp == p || m.b_col == p) m = {};
+    for (auto *tab : {ctx->lane_miss, ctx->list_miss})
+        for (int i = 0; i < 8; ++i)
+            if (tab[i].a_rp == p || tab[i].a_col == p || tab[i].b_rp == p || tab[i].b_col == p) tab[i] = {};
     b.s = s;
     cache_put(ctx, b);
     if (ctx->cache_bytes > kCacheMax) {
@@ -866,6 +867,21 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     // (C1: A^2 of the 30^3 torus, 7 x 8 = 56 products a row)
     // (maxrow_b > 0: with an empty B the bound says nothing about a row's entry count)
     const bool all_short = sym_batched && batched && !asym.wide && bound_short;
+    // speculative wide launches: the listed-row launches (symbolic and numeric window rows) are not
+    // queued, as if every row were short; a short-row kernel that lists a row sets a mapped word and
+    // the call reruns with them (C4 lists none: its two launches found empty lists, ~4.5 us each of a
+    // row block's ~217). A triple that listed rows once is remembered and not speculated again
+    // (SLAT_NO_SPEC: never, A/B)
+    static const bool kNoSpec = slat_ab_knob("SLAT_NO_SPEC") != nullptr;
+    auto same = [&](const slat_ctx::LaneMiss &m) {
+        return m.a_rp == A->row_ptr && m.a_col == A->col_idx && m.b_rp == B->row_ptr && m.b_col == B->col_idx &&
+               m.a_nnz == A->nnz && m.b_nnz == B->nnz && m.a_rows == A->n_rows && m.row_begin == row_begin &&
+               m.row_end == row_end;
+    };
+    bool spec = sym_batched && batched && asym.wide && !kNoSpec && !(flags & kFlagNoSpec) && !exact;
+    if (spec)
+        for (const auto &m : ctx->list_miss)
+            if (same(m)) spec = false;
     const size_t hash_lds =
         (size_t)wpb * (dt == SLAT_U32    ? (!batched ? hash_bytes<SemU32>() : short_bytes<SemU32>())
                        : dt == SLAT_SAT64 ? (!batched ? hash_bytes<SemSat64>() : short_bytes<SemSat64>())
@@ -938,12 +954,21 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     const uint64_t maxrow_a = A->max_row_nnz;
     const uint64_t fat_min = slat_fat_min(!ell && (dt != SLAT_F64 || f64any));
     const bool fat = !kNoFat && !tiny && !lane && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= fat_min : maxrow_b > 32);
+    // MODE 4 with the row offsets folded into the two passes (Args::fold_rows): no k_scan_rows launch
+    // (8 us and a kernel boundary of the 30^3 A^6 * A step). Symbolic blocks of R consecutive rows,
+    // G <= 16 * kBlock blocks so the last block's prefix takes one pass (R <= 64: numeric sums a row's
+    // group with one wave). SLAT_NO_FOLD: the scan (A/B)
+    static const bool kNoFold = slat_ab_knob("SLAT_FOLD") == nullptr;
+    const uint64_t fold_r = std::max<uint64_t>(8, (n + kFoldPer * kBlock - 1) / (kFoldPer * kBlock));
+    const bool fold = win_mode == 4 && !fat && !exact && !ablate && !kNoFold && fold_r <= kWave;
+    const uint64_t fold_g = fold ? (n + fold_r - 1) / fold_r : 0;
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (bell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
     const size_t o_bmax = o_fat + fat_b,  // per-block max counts (the symbolic grid)
-        bmax_b = up256((size_t)std::max<uint64_t>(sym_grid.x, (uint64_t)ctx->cu_count * 8) * 4);
-    if ((st = slat_ensure_ws(ctx, o_bmax + bmax_b))) return st;
+        bmax_b = up256((size_t)std::max<uint64_t>(std::max<uint64_t>(sym_grid.x, fold_g), (uint64_t)ctx->cu_count * 8) * 4);
+    const size_t o_bsum = o_bmax + bmax_b, bsum_b = up256(fold_g * 8);  // (folded launches) block sums
+    if ((st = slat_ensure_ws(ctx, o_bsum + bsum_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (pell) {
         a.ell_wq = (uint32_t)wq;
@@ -1150,6 +1175,11 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         return e ? (uint32_t)std::atoi(e) : 2u;
     }();
     unsigned long long *tq = ctx->d_words + 5;
+    // the call's last kernel stores the completion word itself unless fat rows or the stats copy
+    // follow (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
+    static const bool kFusedSignal = slat_ab_knob("SLAT_NO_FUSED_SIGNAL") == nullptr;
+    const bool fused = kFusedSignal && !fat && !a.stats && wait_mode() == 0;
+    spec = spec && fused;  // (the short numeric kernel then ends the call)
     uint32_t sym_blocks = sym_grid.x;  // blocks of the symbolic launch whose maxima the scan reduces
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[0], s));
     if (fat && (st = slat_fat_symbolic(ctx, *fa, asym, idx32))) return failc(st);
@@ -1177,10 +1207,11 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         h1.list_cnt = h2.list_cnt = lc;
         const uint64_t trows = h1.tile_rows ? h1.tile_rows : kWave;
         const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + trows - 1) / trows / wpb + 1, ctx->cu_count * 16ull)));
+        if (spec) h1.spec_flag = ctx->h_out_dev + 3;
         SLAT_HIPC(slat_launch_symbolic_short(idx32, ell, g1, wpb * sym_short_bytes(), s, h1));
         h2.tq = (kDyn & 2u) && asym.wide ? tq : nullptr;  // (single-window rows: a fixed stride)
-        if (all_short) {
-            // (no listed rows)
+        if (all_short || spec) {
+            // (no listed rows, or none expected: spec)
         } else {
             // the listed rows take tickets in wide launches, so a resident grid covers any list (the
             // launch is mostly its dispatch when the list is short: C4 lists none, and 4 096 blocks
@@ -1202,7 +1233,22 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         // single-window launch without fat rows: symbolic leaves per-block max row counts for the
         // scan's last tile (<= 16 per scan thread)
         if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
-        if (win_mode == 4)  // the stored-bitmap pair: symbolic MODE 4 (spgemm_stored.hpp)
+        if (fold) {
+            // symbolic's blocks of fold_r rows; the last one to finish does the scan's work
+            asym.bmax = (uint32_t *)(ws + o_bmax);
+            asym.fold_rows = a.fold_rows = (uint32_t)fold_r;
+            asym.bsum = a.bsum = (unsigned long long *)(ws + o_bsum);
+            asym.done = ctx->d_done;
+            asym.host_out = a.host_out;
+            asym.b_vmax = a.b_vmax;
+            asym.epoch = a.epoch;
+            if (bell && dt != SLAT_F64) {
+                asym.bpart = (const unsigned long long *)(ws + o_part);
+                asym.nbpart = build_ell_blocks(B, a.ell_wq);
+            }
+            a.ncounts = (uint64_t *)(ws + o_abl);
+            SLAT_HIPC(slat_launch_symbolic(4, idx32, ell, dim3((unsigned)fold_g), (size_t)wpb * sym_stored_words(asym.ww) * 4, s, asym));
+        } else if (win_mode == 4)  // the stored-bitmap pair: symbolic MODE 4 (spgemm_stored.hpp)
             SLAT_HIPC(slat_launch_symbolic(4, idx32, ell, sym_grid, (size_t)wpb * sym_stored_words(asym.ww) * 4, s, asym));
         else
             SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
@@ -1211,7 +1257,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
     // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
     const bool bpart = bell && dt != SLAT_F64;
-    if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
+    if (!fold && (st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
                                bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
                                bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch, asym.bmax, sym_blocks, list_next)))
         return failc(st);
@@ -1242,26 +1288,23 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         SLAT_HIPC(launch_num(abl));
         SLAT_HIPC(hipEventRecord(ctx->ev[5], s));
     }
-    // the call's last kernel stores the completion word itself unless fat rows or the stats copy
-    // follow (SLAT_NO_FUSED_SIGNAL: a k_signal launch after it, A/B)
-    static const bool kFusedSignal = slat_ab_knob("SLAT_NO_FUSED_SIGNAL") == nullptr;
-    const bool fused = kFusedSignal && !fat && !a.stats && wait_mode() == 0;
     if (hash) {
         Args h1 = a;
         if (!batched) a.list = h1.list = nullptr;  // f64: MODE 1 does not list; MODE 2 tests each row
         h1.tq = (kDyn & 2u) && hash_mode != 3 ? tq : nullptr;
-        if (all_short && fused) {
+        if ((all_short || spec) && fused) {
             a.seq = h1.seq = ++ctx->done_seq;
             h1.done = ctx->d_done;
         }
+        if (spec) h1.spec_flag = ctx->h_out_dev + 3;
         SLAT_HIPC(slat_launch_numeric(sem, hash_mode, idx32, ell, hash_grid, hash_lds, s, h1));
     }
     a.tq = (kDyn & 2u) && hash && a.wide ? tq : nullptr;  // (single-window rows: a fixed stride)
-    if (fused && !all_short) {
+    if (fused && !all_short && !spec) {
         a.seq = ++ctx->done_seq;
         a.done = ctx->d_done;
     }
-    if (!all_short) SLAT_HIPC(launch_num(a));
+    if (!all_short && !spec) SLAT_HIPC(launch_num(a));
     if (wsplit) slat_dev_free(ctx, wsplit, s);  // stream-ordered: reused only by later work
     if (fat && (st = slat_fat_numeric(ctx, *fa, a, dt, f64any, idx32))) return failc(st);
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[3], s));
@@ -1269,6 +1312,15 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
                                              hipMemcpyDeviceToHost, s));
     hc.mark(6);
     SLAT_HIPC(wait_stream(ctx, s, a.seq));
+    if (spec && ctx->h_out[3]) {
+        // a short-row kernel listed a row: this call is void; again with the listed-row launches
+        ctx->list_miss[ctx->list_miss_next++ % 8] = {A->row_ptr, A->col_idx, B->row_ptr, B->col_idx, A->nnz,
+                                                     B->nnz,     A->n_rows,   row_begin, row_end};
+        (void)failc(SLAT_OK);
+        const slat_status rs = rowblock_impl(ctx, A, row_begin, row_end, B, prep, C, flags | kFlagNoSpec);
+        if (rs == SLAT_OK) ctx->stats.mode |= 64u;
+        return rs;
+    }
     }  // regular pipeline
 #undef SLAT_HIPC
     hc.mark(7);
@@ -1295,7 +1347,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         // exact zeros were dropped: rebuild row_ptr from the per-row actual counts and move rows
         uint64_t *nrp = nullptr;
         SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&nrp, (n + 1) * 8, s));
-        if ((st = slat_launch_scan(ctx, a.counts, n, nrp, s))) return st;
+        if ((st = slat_launch_scan(ctx, fold ? a.ncounts : a.counts, n, nrp, s))) return st;
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         const uint64_t total = ctx->h_out[0];
         maxrow = ctx->h_out[1];
@@ -1341,7 +1393,8 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     S.flops = flops;
     S.capacity = C->capacity;
     S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u) | (run_lane ? 8u : 0u) |
-             (!run_tiny && !run_lane && win_mode == 4 ? 16u : 0u);
+             (!run_tiny && !run_lane && win_mode == 4 ? 16u : 0u) | (!run_tiny && !run_lane && spec ? 32u : 0u) |
+             (!run_tiny && !run_lane && fold ? 128u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;

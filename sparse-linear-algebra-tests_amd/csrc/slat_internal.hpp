@@ -27,6 +27,10 @@ inline const char *slat_ab_knob(const char *name) {
 
 struct slat_hostio;  // the page-locked staging ring and its copy threads (slat_hostio.hip)
 
+// internal call flag (above the public SLAT_FLAG_* bits): the rerun of a void speculative wide
+// launch, which queues the listed-row launches
+constexpr uint32_t kFlagNoSpec = 0x80000000u;
+
 struct slat_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -61,6 +65,11 @@ struct slat_ctx {
         uint64_t a_nnz, b_nnz, a_rows, row_begin, row_end;
     } lane_miss[8] = {};
     uint32_t lane_miss_next = 0;
+    // (A, B, row block) triples whose speculative wide launch (the listed-row launches skipped, as if
+    // every row were short) found a row of the window category: the next call on the same triple
+    // queues the listed-row launches directly instead of running twice
+    LaneMiss list_miss[8] = {};
+    uint32_t list_miss_next = 0;
     unsigned long long *d_status = nullptr;  // scan tile status words (epoch-tagged)
     uint64_t status_cap = 0;                 // tiles d_status holds
     uint32_t scan_epoch = 0;                 // tag of the status / max-row words (22 bits)
