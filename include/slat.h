@@ -122,8 +122,7 @@ typedef struct {
     uint32_t mode;         /* bits: 1 = 32-bit offsets, 2 = B's ELL image, 4 = the one-kernel small path,
                               8 = the lane kernel, 16 = the stored-bitmap numeric pass (MODE 4),
                               32 = a speculative wide launch (no listed-row launches) that held,
-                              64 = a speculative wide launch that listed a row and was rerun,
-                              128 = MODE 4 with the row offsets folded into the passes (no scan) */
+                              64 = a speculative wide launch that listed a row and was rerun */
     uint32_t window_words; /* LDS bitmap words per window */
     uint32_t exact_alloc;  /* 1 if the mid-call-sync path was taken */
     uint32_t dropped_rows; /* rows that lost explicit zeros in the numeric pass */

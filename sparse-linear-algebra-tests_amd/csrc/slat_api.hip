@@ -954,21 +954,12 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     const uint64_t maxrow_a = A->max_row_nnz;
     const uint64_t fat_min = slat_fat_min(!ell && (dt != SLAT_F64 || f64any));
     const bool fat = !kNoFat && !tiny && !lane && (maxrow_a ? (unsigned __int128)maxrow_a * maxrow_b >= fat_min : maxrow_b > 32);
-    // MODE 4 with the row offsets folded into the two passes (Args::fold_rows): no k_scan_rows launch
-    // (8 us and a kernel boundary of the 30^3 A^6 * A step). Symbolic blocks of R consecutive rows,
-    // G <= 16 * kBlock blocks so the last block's prefix takes one pass (R <= 64: numeric sums a row's
-    // group with one wave). SLAT_NO_FOLD: the scan (A/B)
-    static const bool kNoFold = slat_ab_knob("SLAT_FOLD") == nullptr;
-    const uint64_t fold_r = std::max<uint64_t>(8, (n + kFoldPer * kBlock - 1) / (kFoldPer * kBlock));
-    const bool fold = win_mode == 4 && !fat && !exact && !ablate && !kNoFold && fold_r <= kWave;
-    const uint64_t fold_g = fold ? (n + fold_r - 1) / fold_r : 0;
     // k_build_ell's per-block B-value partials (u32), reduced by k_scan_rows
     const size_t o_part = o_lc + lc_b, part_b = (bell && dt != SLAT_F64) ? 4096 * 8 : 0;
     const size_t o_fat = o_part + part_b, fat_b = fat ? slat_fat_ws(n) : 0;
     const size_t o_bmax = o_fat + fat_b,  // per-block max counts (the symbolic grid)
-        bmax_b = up256((size_t)std::max<uint64_t>(std::max<uint64_t>(sym_grid.x, fold_g), (uint64_t)ctx->cu_count * 8) * 4);
-    const size_t o_bsum = o_bmax + bmax_b, bsum_b = up256(fold_g * 8);  // (folded launches) block sums
-    if ((st = slat_ensure_ws(ctx, o_bsum + bsum_b))) return st;
+        bmax_b = up256((size_t)std::max<uint64_t>(sym_grid.x, (uint64_t)ctx->cu_count * 8) * 4);
+    if ((st = slat_ensure_ws(ctx, o_bmax + bmax_b))) return st;
     uint8_t *ws = (uint8_t *)ctx->ws;
     if (pell) {
         a.ell_wq = (uint32_t)wq;
@@ -1233,22 +1224,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         // single-window launch without fat rows: symbolic leaves per-block max row counts for the
         // scan's last tile (<= 16 per scan thread)
         if (!fat && sym_grid.x <= 16u * kScanThreads) asym.bmax = (uint32_t *)(ws + o_bmax);
-        if (fold) {
-            // symbolic's blocks of fold_r rows; the last one to finish does the scan's work
-            asym.bmax = (uint32_t *)(ws + o_bmax);
-            asym.fold_rows = a.fold_rows = (uint32_t)fold_r;
-            asym.bsum = a.bsum = (unsigned long long *)(ws + o_bsum);
-            asym.done = ctx->d_done;
-            asym.host_out = a.host_out;
-            asym.b_vmax = a.b_vmax;
-            asym.epoch = a.epoch;
-            if (bell && dt != SLAT_F64) {
-                asym.bpart = (const unsigned long long *)(ws + o_part);
-                asym.nbpart = build_ell_blocks(B, a.ell_wq);
-            }
-            a.ncounts = (uint64_t *)(ws + o_abl);
-            SLAT_HIPC(slat_launch_symbolic(4, idx32, ell, dim3((unsigned)fold_g), (size_t)wpb * sym_stored_words(asym.ww) * 4, s, asym));
-        } else if (win_mode == 4)  // the stored-bitmap pair: symbolic MODE 4 (spgemm_stored.hpp)
+        if (win_mode == 4)  // the stored-bitmap pair: symbolic MODE 4 (spgemm_stored.hpp)
             SLAT_HIPC(slat_launch_symbolic(4, idx32, ell, sym_grid, (size_t)wpb * sym_stored_words(asym.ww) * 4, s, asym));
         else
             SLAT_HIPC(slat_launch_symbolic(0, idx32, ell, sym_grid, sym_lds, s, asym));
@@ -1257,7 +1233,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     if (timing) SLAT_HIPC(hipEventRecord(ctx->ev[1], s));
     // (u32 / Sat64 with the ELL copy: the scan also reduces k_build_ell's B-value partials for numeric)
     const bool bpart = bell && dt != SLAT_F64;
-    if (!fold && (st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
+    if ((st = slat_launch_scan(ctx, a.counts, n, C->row_ptr, s,
                                bpart ? (const unsigned long long *)(ws + o_part) : nullptr,
                                bpart ? build_ell_blocks(B, a.ell_wq) : 0u, a.epoch, asym.bmax, sym_blocks, list_next)))
         return failc(st);
@@ -1347,7 +1323,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         // exact zeros were dropped: rebuild row_ptr from the per-row actual counts and move rows
         uint64_t *nrp = nullptr;
         SLAT_HIP(ctx, slat_dev_alloc(ctx, (void **)&nrp, (n + 1) * 8, s));
-        if ((st = slat_launch_scan(ctx, fold ? a.ncounts : a.counts, n, nrp, s))) return st;
+        if ((st = slat_launch_scan(ctx, a.counts, n, nrp, s))) return st;
         SLAT_HIP(ctx, hipStreamSynchronize(s));
         const uint64_t total = ctx->h_out[0];
         maxrow = ctx->h_out[1];
@@ -1393,8 +1369,7 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     S.flops = flops;
     S.capacity = C->capacity;
     S.mode = (idx32 ? 1u : 0u) | (ell ? 2u : 0u) | (run_tiny ? 4u : 0u) | (run_lane ? 8u : 0u) |
-             (!run_tiny && !run_lane && win_mode == 4 ? 16u : 0u) | (!run_tiny && !run_lane && spec ? 32u : 0u) |
-             (!run_tiny && !run_lane && fold ? 128u : 0u);
+             (!run_tiny && !run_lane && win_mode == 4 ? 16u : 0u) | (!run_tiny && !run_lane && spec ? 32u : 0u);
     S.window_words = a.ww;
     S.exact_alloc = exact ? 1u : 0u;
     S.dropped_rows = (uint32_t)drops;

@@ -171,17 +171,6 @@ struct Args {
     // reruns the call with them. k_symbolic_short gives such a row 0 outputs, so the scan and the
     // numeric batches stay inside C's bound-sized arrays
     unsigned long long *spec_flag;
-    // single-window MODE 4 launches with the row offsets folded into the two passes (no k_scan_rows;
-    // 0: the scan). k_symbolic's block b counts rows [b * fold_rows, (b + 1) * fold_rows) and stores
-    // their sum at bsum[b] (and max at bmax[b]); the last block to finish turns bsum into exclusive
-    // prefixes, stores nnz and the max row in host_out[0] / [1] and reduces k_build_ell's B-value
-    // partials (bpart, nbpart) into b_vmax. k_numeric takes row r's offset as bsum[r / fold_rows] plus
-    // the counts before it in its group, stores row_ptr[r + 1], and its zero-dropped counts in ncounts
-    uint32_t fold_rows;
-    uint32_t nbpart;
-    unsigned long long *bsum;
-    const unsigned long long *bpart;
-    uint64_t *ncounts;
 };
 
 __device__ __forceinline__ bool fat_row(const Args &p, uint64_t row) { return p.fr_mark && p.fr_mark[row]; }
@@ -215,22 +204,6 @@ __device__ __forceinline__ void signal_done(const Args &p) {
         __hip_atomic_store(p.done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&p.host_out[7], p.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-}
-
-// (thread 0 of each block, after the block's results are stored write-through and waited for)
-// whether this block is the launch's last to finish: the two-level count of signal_done, left at 0 by
-// the last block. Relaxed: a release fence here writes back the XCD's L2, dirty with the launch's
-// stored bitmaps (the fold's first version: symbolic 40 -> 161 us); the results it hands over are
-// sc1 (write-through) stores drained by a vmcnt(0) before the count, read back with sc1 loads
-__device__ __forceinline__ bool last_block_done(unsigned long long *done) {
-    const uint32_t G = gridDim.x, g = blockIdx.x % kDoneGroups;
-    const uint32_t groups = min(G, kDoneGroups), members = (G - g + kDoneGroups - 1) / kDoneGroups;
-    unsigned long long *gw = done + (size_t)kDoneStride * (g + 1);
-    if (__hip_atomic_fetch_add(gw, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != members - 1) return false;
-    __hip_atomic_store(gw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != groups - 1) return false;
-    __hip_atomic_store(done, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
 }
 
 // The call's max row count in the one-kernel paths (k_tiny, k_lane), two-level like the done count:
@@ -1714,15 +1687,10 @@ void k_symbolic(Args p) {
     // the block's max row count (p.bmax): LDS max of the waves' maxima; the last wave to finish
     // stores it (no block barrier at the end, no global atomics on one word)
     __shared__ uint32_t s_bmax, s_bdone;
-    __shared__ unsigned long long s_bsum;
     if (p.bmax) {
-        if (threadIdx.x == 0) {
-            s_bmax = s_bdone = 0;
-            s_bsum = 0;
-        }
+        if (threadIdx.x == 0) s_bmax = s_bdone = 0;
         __syncthreads();
     }
-    uint64_t fsum = 0;  // (folded launches) the wave's count sum
     const bool listed = MODE == 2 && p.list != nullptr;  // rows of this category, listed by k_symbolic_short
     const uint64_t nit = listed ? list_len(p) : p.nrows;
     // a wave with no listed row leaves before touching LDS (C4 lists none: the launch is then
@@ -1746,12 +1714,7 @@ void k_symbolic(Args p) {
             if (r < nit && lane < 2) pre = p.a_rp[r + lane];
     };
     if constexpr (MODE == 4) {
-        if (p.fold_rows) {  // rows [b * fold_rows, (b + 1) * fold_rows), the waves taking every 4th
-            const uint64_t r0 = (uint64_t)blockIdx.x * p.fold_rows;
-            symbolic_rows_stored<I>(p, smem, wv, r0 + wv, kWpb, min(nit, r0 + p.fold_rows), mx, flops, fsum);
-        } else {
-            symbolic_rows_stored<I>(p, smem, wv, (uint64_t)blockIdx.x * kWpb + wv, stride, nit, mx, flops, fsum);
-        }
+        symbolic_rows_stored<I>(p, smem, wv, (uint64_t)blockIdx.x * kWpb + wv, stride, mx, flops);
     } else {
     prefetch((uint64_t)blockIdx.x * kWpb + wv);
     for (uint64_t it = (uint64_t)blockIdx.x * kWpb + wv; it < nit; it = dyn ? tq.resolve(pend) : it + stride) {
@@ -1772,11 +1735,6 @@ void k_symbolic(Args p) {
     }
     if (p.stats && lane == 0 && flops)
         atomicAdd(&p.shards[((blockIdx.x * kWpb + wv) % kShards) * kShardStride + 3], flops);
-    if constexpr (MODE == 4)
-        if (p.fold_rows) {
-            fold_block_end(p, mx, fsum, s_bmax, s_bsum);
-            return;
-        }
     if (p.bmax && lane == 0) {
         atomicMax(&s_bmax, (uint32_t)(mx < 0xFFFFFFFFull ? mx : 0xFFFFFFFFull));
         if (atomicAdd(&s_bdone, 1u) == (uint32_t)kWpb - 1) p.bmax[blockIdx.x] = atomicMax(&s_bmax, 0u);

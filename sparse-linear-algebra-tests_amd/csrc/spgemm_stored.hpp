@@ -114,43 +114,19 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
     // mask (bm), lane 5 its fat mark (fm). Each load sits bare in its branch, into a variable of its
     // own type: a conversion inside the branch made the wave wait for the load there (vmcnt(0), so
     // for every load in flight, the groups included)
-    // Folded launches (p.fold_rows = R): lane 2 loads the exclusive prefix of the row's group of R
-    // rows (bsum) instead of its C slice, and lane j the count of the group's j-th row for j <= r % R
-    // (cn): the slice is [bsum + the counts before r, + r's count)
     struct Ahead {
         uint64_t bd;
         uint32_t bm;
         uint32_t fm;
-        uint32_t cn;
     };
-    const uint32_t R = p.fold_rows;
     auto ahead = [&](uint64_t r, Ahead &h) {
         h.bd = 0;
         h.bm = 0;
         h.fm = 0;
-        h.cn = 0;
         if (r < nit) {
-            if (R) {
-                const uint64_t g = r / R, j = r - g * R;
-                if (lane < 2) h.bd = p.a_rp[r + (uint64_t)lane];
-                if (lane == 2) h.bd = p.bsum[g];
-                if ((uint32_t)lane <= j) h.cn = (uint32_t)p.counts[g * R + (uint64_t)lane];
-            } else {
-                if (lane < 4) h.bd = (lane < 2 ? p.a_rp : (const uint64_t *)p.c_rp)[r + (uint64_t)(lane & 1)];
-            }
+            if (lane < 4) h.bd = (lane < 2 ? p.a_rp : (const uint64_t *)p.c_rp)[r + (uint64_t)(lane & 1)];
             if (lane == 4) h.bm = p.smask[r];
             if (lane == 5 && p.fr_mark) h.fm = p.fr_mark[r];
-        }
-    };
-    // a row's C slice from its bounds
-    auto slice = [&](const Ahead &h, uint64_t r, uint64_t &ob, uint64_t &oe) {
-        if (R) {
-            const uint32_t j = (uint32_t)(r - r / R * R);
-            ob = readlane_u64(h.bd, 2) + wave_sum_u32((uint32_t)lane < j ? h.cn : 0u);
-            oe = ob + readlane_u32(h.cn, (int)j);
-        } else {
-            ob = readlane_u64(h.bd, 2);
-            oe = readlane_u64(h.bd, 3);
         }
     };
 
@@ -159,9 +135,7 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
     ahead(first, nxt);
     for (uint64_t row = first; row < nit; row += stride) {
         const I a0 = (I)readlane_u64(nxt.bd, 0), a1 = (I)readlane_u64(nxt.bd, 1);
-        uint64_t ob, oe;
-        slice(nxt, row, ob, oe);
-        if (R && lane == 0) p.c_rp[row + 1] = oe;  // (symbolic's block 0 stored row_ptr[0])
+        const uint64_t ob = readlane_u64(nxt.bd, 2), oe = readlane_u64(nxt.bd, 3);
         const uint32_t bmask = readlane_u32(nxt.bm, 4);
         if (readlane_u32(nxt.fm, 5) != 0) {  // the fat-row kernels' row
             ahead(row + stride, nxt);
@@ -422,8 +396,7 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
         }
         if (!issued) ahead(row + stride, nxt);
         const uint32_t rz = wave_sum_u32(zeros);
-        // (folded launches: the counts stay the structural ones, which later rows' slices are taken from)
-        if (lane == 0) (R ? p.ncounts : p.counts)[row] = out_pos - ob - rz;
+        if (lane == 0) p.counts[row] = out_pos - ob - rz;
         zrows += rz ? 1u : 0u;
     }
     add_zero_rows(&p.host_out[2], zrows, p.seq != 0);
@@ -448,10 +421,10 @@ __host__ __device__ constexpr uint32_t sym_stored_words(uint32_t ww) { return ((
 
 template <typename I>
 __device__ __forceinline__ void symbolic_rows_stored(const Args &p, uint32_t *smem, int wv, uint64_t first,
-                                                     uint64_t stride, uint64_t nit, uint64_t &mx,
-                                                     unsigned long long &flops, uint64_t &sum) {
+                                                     uint64_t stride, uint64_t &mx, unsigned long long &flops) {
     constexpr uint32_t kSeg = kWave * kSymQ;
     const int lane = lane_id();
+    const uint64_t nit = p.nrows;
     const uint32_t ww = p.ww;
     uint32_t *L0 = smem + (size_t)wv * sym_stored_words(ww);
     uint32_t *queue = L0 + ((ww + kWave + 3) & ~3u);  // kSymQueue items + a sink entry
@@ -560,76 +533,7 @@ __device__ __forceinline__ void symbolic_rows_stored(const Args &p, uint32_t *sm
         if (p.stats) flops += wave_sum_u32(nprod);
         if (lane == 0) p.counts[row] = cnt;
         mx = max(mx, cnt);
-        sum += cnt;
         wave_sync();
-    }
-}
-
-// The end of a k_symbolic block of a folded launch (p.fold_rows): the block's count sum and max at
-// bsum[b] / bmax[b]; the last block to finish replaces bsum[0, G) by its exclusive prefix (G <= 16 *
-// kBlock blocks: 16 per thread), stores nnz and the max row into the mapped host words, and reduces
-// k_build_ell's B-value partials into b_vmax, which is what k_scan_rows did between the passes
-constexpr uint32_t kFoldPer = 16;
-__device__ __forceinline__ void fold_block_end(const Args &p, uint64_t mx, uint64_t sum, uint32_t &s_max,
-                                               unsigned long long &s_sum) {
-    __shared__ uint32_t s_last;
-    __shared__ unsigned long long s_ws[kBlock / kWave];
-    const int lane = lane_id(), w = threadIdx.x / kWave;
-    // (s_sum / s_max: the block's words, zeroed at kernel start before its first barrier)
-    if (lane == 0) {
-        atomicAdd(&s_sum, (unsigned long long)sum);
-        atomicMax(&s_max, (uint32_t)min<uint64_t>(mx, 0xFFFFFFFFull));
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(&p.bsum[blockIdx.x], s_sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&p.bmax[blockIdx.x], s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0);  // (both stores reached the coherent level before the count)
-        s_last = last_block_done(p.done) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    const uint32_t G = gridDim.x, t = threadIdx.x;
-    unsigned long long v[kFoldPer], run = 0;
-    uint32_t m = 0;
-    sfor<kFoldPer>([&](auto I_) {
-        const uint32_t e = t * kFoldPer + I_;
-        v[I_] = e < G ? __hip_atomic_load(&p.bsum[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        m = max(m, e < G ? __hip_atomic_load(&p.bmax[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u);
-    });
-    sfor<kFoldPer>([&](auto I_) { run += v[I_]; });
-    const unsigned long long wi = wave_incl_scan_u64(run);
-    m = wave_max_u32(m);
-    if (lane == kWave - 1) s_ws[w] = wi;
-    if (lane == 0) atomicMax(&s_max, m);
-    __syncthreads();
-    unsigned long long pre = wi - run, tot = 0;
-    for (int k = 0; k < kBlock / kWave; ++k) {
-        pre += k < w ? s_ws[k] : 0ull;
-        tot += s_ws[k];
-    }
-    sfor<kFoldPer>([&](auto I_) {
-        const uint32_t e = t * kFoldPer + I_;
-        if (e < G) p.bsum[e] = pre;
-        pre += v[I_];
-    });
-    if (t == 0) {
-        __hip_atomic_store(&p.host_out[0], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&p.host_out[1], (unsigned long long)s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (w == 1 && p.bpart) {  // k_build_ell's B-value partials, as k_scan_rows' tile 0 reduces them
-        uint32_t bx = 0, bn = 0;
-        for (uint32_t i = lane; i < p.nbpart; i += kWave) {
-            const unsigned long long q = p.bpart[i];
-            bx = max(bx, (uint32_t)q);
-            bn = max(bn, (uint32_t)(q >> 32));
-        }
-        bx = wave_max_u32(bx);
-        bn = wave_max_u32(bn);
-        if (lane == 0) {
-            p.b_vmax[kVMaxWord] = ((unsigned long long)p.epoch << 32) | bx;
-            p.b_vmax[kVMinInvWord] = ((unsigned long long)p.epoch << 32) | bn;
-        }
     }
 }
 
