@@ -1197,7 +1197,13 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
         h1.list = h2.list = all_short ? nullptr : (uint32_t *)(ws + o_l1);
         h1.list_cnt = h2.list_cnt = lc;
         const uint64_t trows = h1.tile_rows ? h1.tile_rows : kWave;
-        const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + trows - 1) / trows / wpb + 1, ctx->cu_count * 16ull)));
+        // (at most 10 blocks per CU, ~1.7 rounds of the 6 resident: C4 1.288 -> 1.272 ms against 16,
+        // one eighth and R-MAT 2^16 A^2 within 1 %, profiles/r06_short_bpc_sweep.txt; SLAT_SHORT_BPC: A/B)
+        static const uint64_t kShortBpc = [] {
+            const char *e = slat_ab_knob("SLAT_SHORT_BPC");
+            return e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 10ull;
+        }();
+        const dim3 g1((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + trows - 1) / trows / wpb + 1, ctx->cu_count * kShortBpc)));
         if (spec) h1.spec_flag = ctx->h_out_dev + 3;
         SLAT_HIPC(slat_launch_symbolic_short(idx32, ell, g1, wpb * sym_short_bytes(), s, h1));
         h2.tq = (kDyn & 2u) && asym.wide ? tq : nullptr;  // (single-window rows: a fixed stride)
