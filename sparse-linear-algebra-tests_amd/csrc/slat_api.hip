@@ -752,7 +752,9 @@ static slat_status rowblock_impl(slat_ctx *ctx, const slat_csr_view *A, uint64_t
     Args asym = a;
     pick_window(ncols, kWave, 1984, asym.ww, asym.wide);
     pick_window(ncols, kWave, 1984, a.ww, a.wide);
-    a.area = 896 * 6;  // rank slots per wave: 896 narrow (u32 + u16) slots; 3 blocks/CU at the 30^3 window
+    // rank slots per wave: 896 narrow (u32 + u16) slots and MODE 4's 64 sink slots; 3 blocks/CU at the
+    // 30^3 window (MODE 0 takes all 960 as slots)
+    a.area = 960 * 6;
     // Wide launches (columns beyond one window): short rows take the per-wave LDS hash table
     // (MAGNUS's small-row category); the rest keep row-span windows, made small so the shared
     // region stays small: symbolic 1024 words (the hash keys' size), numeric 256 words.

@@ -41,7 +41,10 @@ struct StItem {
 };
 
 // one rank chunk's accumulate: a group of four columns and their products, rank lookups first, then
-// the adds of the columns inside [r0, r0 + nch)
+// the adds. A column outside [r0, r0 + nch) (another chunk's, or padding) adds into its lane's own
+// sink slot (slot sink + lane, past the chunk's slots) instead of taking a branch: the branch cost an
+// exec save, a skip and a restore per product (one sink slot for every lane would serialise the
+// instruction on its address)
 template <typename Sem, bool NW>
 struct StAcc {
     using S = typename Sem::S;
@@ -50,22 +53,20 @@ struct StAcc {
     uint32_t ww;
     void *vals;
     uint16_t *cols;
-    uint32_t r0, nch;
+    uint32_t r0, nch, sink;
     __device__ __forceinline__ void operator()(const uint4 &c, const Quad<S> &pr) const {
         const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
         uint2 w[4];
         sfor<4>([&](auto E) { w[E] = W[min(cc[E] >> 5, ww)]; });
+        const uint32_t ls = sink + (uint32_t)lane_id();
         sfor<4>([&](auto E) {
             const uint32_t r = __builtin_popcount(__builtin_amdgcn_ubfe(w[E].x, 0u, cc[E])) + (w[E].y - r0);
-            // (a branch, not a spare slot for the rest: the padding of one instruction's lanes all
-            // hitting one LDS address serialises the instruction)
-            if (r < nch) {
-                if constexpr (NW)
-                    atomicAdd((uint32_t *)vals + r, (uint32_t)pr.v[E]);
-                else
-                    Sem::acc((V *)vals, r, pr.v[E]);
-                cols[r] = (uint16_t)cc[E];
-            }
+            const uint32_t rr = r < nch ? r : ls;
+            if constexpr (NW)
+                atomicAdd((uint32_t *)vals + rr, (uint32_t)pr.v[E]);
+            else
+                Sem::acc((V *)vals, rr, pr.v[E]);
+            cols[rr] = (uint16_t)cc[E];
         });
     }
     __device__ __forceinline__ void multi(const uint4 *c, const Quad<S> *pr) const {
@@ -87,7 +88,8 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
     uint8_t *region = smem8 + (size_t)wv * lay.bytes;
     uint2 *W = (uint2 *)region;
     uint8_t *slots = region + lay.off_slots;
-    const uint32_t cap_n = p.area / 6, cap_w = p.area / (uint32_t)(sizeof(V) * Sem::kSlots + 2);
+    // rank slots per chunk, after kWave sink slots (StAcc) are set aside
+    const uint32_t cap_n = p.area / 6 - kWave, cap_w = p.area / (uint32_t)(sizeof(V) * Sem::kSlots + 2) - kWave;
     Item *queue = (Item *)slots;  // kStQueue items + a sink entry, zero again before any slot is used
 
     uint32_t bvmax = 0xFFFFFFFFu;
@@ -312,8 +314,8 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
                 constexpr uint32_t kVW = NW ? 1 : Sem::kSlots;
                 using PS = std::conditional_t<NW, SemNarrowT<S>, Sem>;
                 const uint32_t cap = NW ? cap_n : cap_w;
-                VS *vals = (VS *)slots;
-                uint16_t *cols = (uint16_t *)(slots + (size_t)cap * kVW * sizeof(VS));
+                VS *vals = (VS *)slots;  // cap slots, then the kWave sink slots
+                uint16_t *cols = (uint16_t *)(slots + (size_t)(cap + kWave) * kVW * sizeof(VS));
                 // emit of one chunk at the row's slice, coalesced, already sorted; the slots are left zero
                 auto emit = [&](uint32_t nch) {
                     wave_sync();
@@ -351,7 +353,7 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
                     // chunk 0 (peeled: in a loop the compiler hoists all 48 groups' rank addresses out of
                     // it and spills them)
                     const uint32_t nch = min(cap, wcnt);
-                    const StAcc<Sem, NW> acc{W, p.ww, vals, cols, 0u, nch};
+                    const StAcc<Sem, NW> acc{W, p.ww, vals, cols, 0u, nch, cap};
                     sfor<kQ>([&](auto Q) {
                         if (Q * kWave < seg_n) acc(cq[Q], splat4(PS::prod(aq[Q], bv0)));
                     });
@@ -374,9 +376,15 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
                 }
                 for (; r0 < wcnt; r0 += cap) {
                     const uint32_t nch = min(cap, wcnt - r0);
-                    walk(StAcc<Sem, NW>{W, p.ww, vals, cols, r0, nch}, a0);
+                    walk(StAcc<Sem, NW>{W, p.ww, vals, cols, r0, nch, cap}, a0);
                     emit(nch);
                 }
+                // the lane's sink slot back to zero: the next row may take the other slot layout (narrow
+                // or wide), whose value slots overlap these bytes
+#pragma unroll
+                for (uint32_t w = 0; w < kVW; ++w) vals[(cap + (uint32_t)lane) * kVW + w] = VS(0);
+                cols[cap + (uint32_t)lane] = 0;
+                wave_sync();
             };
 #ifdef SLAT_ST_ONLY
             if constexpr (Sem::kNarrowable) run(std::bool_constant<SLAT_ST_ONLY / 2>{}, std::bool_constant<SLAT_ST_ONLY % 2>{}); else
