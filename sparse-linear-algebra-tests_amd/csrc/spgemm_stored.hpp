@@ -508,8 +508,12 @@ __device__ __forceinline__ void symbolic_rows_stored(const Args &p, uint32_t *sm
                     const uint32_t wd = cc[E] >> 5;
                     atomicOr(&L0[wd < ww ? wd : ww + (uint32_t)lane], 1u << (cc[E] & 31));
                     blk |= 1u << ((cc[E] >> 11) & 31);
-                    if (p.stats) nprod += cc[E] != kSent ? 1u : 0u;
                 });
+            };
+            // the product count for the stats, outside the bit loop: a predicated count inside it
+            // costs three VALU per slot even when no stats are asked for
+            auto live = [](const uint4 &c) {
+                return (uint32_t)(c.x != kSent) + (c.y != kSent) + (c.z != kSent) + (c.w != kSent);
             };
             sfor<kSymQ>([&](auto Q) {
                 if (Q * kWave < sn) bits(cq[Q]);
@@ -517,10 +521,17 @@ __device__ __forceinline__ void symbolic_rows_stored(const Args &p, uint32_t *sm
             sfor<kSymTail>([&](auto T) {
                 if (T * kWave < off) bits(ct[T]);
             });
+            if (p.stats) {  // launch-uniform branch
+                sfor<kSymQ>([&](auto Q) { nprod += live(cq[Q]); });
+                sfor<kSymTail>([&](auto T) { nprod += live(ct[T]); });
+            }
             if (ovf)  // more tail groups than the queue: each entry walks its own
                 sfor<kSymQ>([&](auto Q) {
                     if (cq[Q].w != kSent)
-                        walk_brow<SemNone, true, false, I>(p, kq[Q], 0u, 1, [&](uint4 c, const Quad<uint32_t> &) { bits(c); });
+                        walk_brow<SemNone, true, false, I>(p, kq[Q], 0u, 1, [&](uint4 c, const Quad<uint32_t> &) {
+                            bits(c);
+                            if (p.stats) nprod += live(c);
+                        });
                 });
         }
         wave_sync();
