@@ -44,8 +44,11 @@ struct StItem {
 // the adds. A column outside [r0, r0 + nch) (another chunk's, or padding) adds into its lane's own
 // sink slot (slot sink + lane, past the chunk's slots) instead of taking a branch: the branch cost an
 // exec save, a skip and a restore per product (one sink slot for every lane would serialise the
-// instruction on its address)
-template <typename Sem, bool NW>
+// instruction on its address). FIRST (rank chunk 0, r0 = 0): a rank past the chunk is either past the
+// row (padding: 2^31 and up) or, when the row has more chunks, at least cap, so min(rank, sink + lane)
+// takes the place of the compare and select: such a rank lands in its own lane's sink slot or in
+// another lane's (all of them cleared at the row's end)
+template <typename Sem, bool NW, bool FIRST = false>
 struct StAcc {
     using S = typename Sem::S;
     using V = typename Sem::V;
@@ -61,7 +64,7 @@ struct StAcc {
         const uint32_t ls = sink + (uint32_t)lane_id();
         sfor<4>([&](auto E) {
             const uint32_t r = __builtin_popcount(__builtin_amdgcn_ubfe(w[E].x, 0u, cc[E])) + (w[E].y - r0);
-            const uint32_t rr = r < nch ? r : ls;
+            const uint32_t rr = FIRST ? min(r, ls) : r < nch ? r : ls;
             if constexpr (NW)
                 atomicAdd((uint32_t *)vals + rr, (uint32_t)pr.v[E]);
             else
@@ -342,7 +345,7 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
                     wave_sync();
                 };
                 // the entries [from, a1) walked from memory into rank chunk [r0, r0 + nch)
-                auto walk = [&](const StAcc<Sem, NW> &acc, I from) {
+                auto walk = [&](const auto &acc, I from) {
                     if (from < a1) {
                         RowWalker<Sem, I, true, true> rw(p, from, a1);
                         rw.template each_group<true, PS, UNI>(acc, bv0);
@@ -353,7 +356,7 @@ __device__ __forceinline__ void numeric_rows_stored(const Args &p, uint8_t *smem
                     // chunk 0 (peeled: in a loop the compiler hoists all 48 groups' rank addresses out of
                     // it and spills them)
                     const uint32_t nch = min(cap, wcnt);
-                    const StAcc<Sem, NW> acc{W, p.ww, vals, cols, 0u, nch, cap};
+                    const StAcc<Sem, NW, true> acc{W, p.ww, vals, cols, 0u, nch, cap};
                     sfor<kQ>([&](auto Q) {
                         if (Q * kWave < seg_n) acc(cq[Q], splat4(PS::prod(aq[Q], bv0)));
                     });
