@@ -509,7 +509,8 @@ __device__ __forceinline__ void symbolic_rows_stored(const Args &p, uint32_t *sm
                 const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
                 sfor<4>([&](auto E) {
                     const uint32_t wd = cc[E] >> 5;
-                    atomicOr(&L0[wd < ww ? wd : ww + (uint32_t)lane], 1u << (cc[E] & 31));
+                    // (a padding column's word is past ww + 63: min sends it to the lane's sink word)
+                    atomicOr(&L0[min(wd, ww + (uint32_t)lane)], 1u << (cc[E] & 31));
                     blk |= 1u << ((cc[E] >> 11) & 31);
                 });
             };
