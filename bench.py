@@ -88,7 +88,12 @@ def load_pmc(workload: str):
     (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, tools/pmc_headline.py), and its
     file name; the bench itself cannot run under --pmc and time at once."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]*_pmc_{workload}.json")))
+    # by round, then within a round the closing records ("final...") after the others ("mid...")
+    def key(path):
+        tag = os.path.basename(path).split("_pmc_")[0]
+        return (int(tag[1:3]), 1 if "final" in tag else 0, tag)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]*_pmc_{workload}.json")), key=key)
     if not files:
         return None, None
     with open(files[-1]) as f:
