@@ -148,7 +148,8 @@ def e2e_leg(ctx, P, A, steps: int):
         el = timed_steps(fn, steps, 1, ctx.sync)
         out[name] = (el / steps * 1e3, nnz[0] * steps / el / 1e9)
     # the same pageable call in a process whose malloc keeps freed arrays in its heap (glibc's
-    # mmap_max = 0; jemalloc / mimalloc, common Rust allocators, do so by default): each call's fresh
+    # mmap_max = 0, as an opted-in jemalloc / mimalloc would; a std Rust binary uses the system
+    # allocator, so the pageable figure above is the default caller's): each call's fresh
     # output arrays then reuse the previous call's pages instead of a new mmap whose first touch and
     # munmap cost this VM ~7 ms per 47 MB array each (profiles/r05_e2e_os_costs.txt). A child process,
     # since the tunable is read at process start
